@@ -1,0 +1,547 @@
+// Preprocess kernels for gfx950: CLAHE (YCrCb luma), k x k median, and the
+// fused CLAHE+median pass used by the default chain.
+//
+// Reference interface: src/preprocess/ops/clahe_dehaze.py:13-32 (CLAHEDehaze)
+// and src/preprocess/ops/median_derain.py:10-14 (MedianDerain).  The
+// arithmetic those ops delegate to OpenCV is restated here:
+//   * BGR<->YCrCb 8U: 14-bit fixed point (common.h)
+//   * cv::CLAHE 8UC1: per-tile 256-bin histogram, integer clip +
+//     redistribution, float CDF LUT, float bilinear blend of 4 tile LUTs
+//     (cvRound = round-half-even).  Compiled with -ffp-contract=off so the
+//     blend rounds exactly like the scalar C++.
+//   * cv::medianBlur 8UC3: exact per-channel median, BORDER_REPLICATE.
+//
+// HBM layout: frames are B x H x pitch bytes (interleaved BGR).  The LUT
+// workspace is B x tiles^2 x 256 u8 (16 KB per frame at 8x8).
+#include "common.h"
+
+namespace rv {
+
+struct ClaheGeo {
+  int tiles;       // tiles per axis
+  int tw, th;      // tile size in the (possibly reflect-101 extended) image
+  int clip_limit;  // integer clip (0 = no clipping)
+  float lut_scale; // 255.f / (tw*th)
+  float inv_tw, inv_th;
+};
+
+// cv::CLAHE_Impl::apply geometry (imgproc/src/clahe.cpp): when either axis
+// is not divisible by the grid, BOTH axes are extended by
+// tiles - (n % tiles) (a full extra tile-row of padding on a divisible axis).
+static ClaheGeo make_geo(int H, int W, int tiles, double clip) {
+  ClaheGeo g;
+  g.tiles = tiles;
+  if (W % tiles == 0 && H % tiles == 0) {
+    g.tw = W / tiles;
+    g.th = H / tiles;
+  } else {
+    g.tw = (W + tiles - (W % tiles)) / tiles;
+    g.th = (H + tiles - (H % tiles)) / tiles;
+  }
+  int area = g.tw * g.th;
+  g.lut_scale = 255.0f / (float)area;
+  g.clip_limit = 0;
+  if (clip > 0.0) {
+    g.clip_limit = (int)(clip * area / 256);
+    if (g.clip_limit < 1) g.clip_limit = 1;
+  }
+  g.inv_tw = 1.0f / (float)g.tw;
+  g.inv_th = 1.0f / (float)g.th;
+  return g;
+}
+
+// ---------------------------------------------------------------------------
+// Kernel A: per (tile, frame) histogram of Y -> clip -> redistribute -> LUT.
+// One 256-thread workgroup per tile; 4 per-wave LDS histograms cut atomic
+// contention on low-contrast tiles.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restrict__ in,
+                                                        uint8_t* __restrict__ lut, int H, int W,
+                                                        int pitch, ClaheGeo g) {
+  __shared__ int hist[4][256];
+  __shared__ int scan[256];
+  __shared__ int wsum[4];
+  const int t = threadIdx.x;
+  const int wave = t >> 6;
+  const int tile = blockIdx.x;
+  const int b = blockIdx.y;
+  const int ty = tile / g.tiles, tx = tile - (tile / g.tiles) * g.tiles;
+  const int x0 = tx * g.tw, y0 = ty * g.th;
+  const uint8_t* frame = in + (size_t)b * H * pitch;
+
+  for (int i = t; i < 4 * 256; i += 256) (&hist[0][0])[i] = 0;
+  __syncthreads();
+
+  const bool inside = (x0 + g.tw <= W) && (y0 + g.th <= H);
+  const bool vec = inside && (g.tw % 4 == 0) && (pitch % 4 == 0) &&
+                   ((((uintptr_t)frame) + (uintptr_t)x0 * 3) % 4 == 0);
+  int* h = hist[wave];
+  if (vec) {
+    const int groups = g.tw >> 2;
+    const int total = groups * g.th;
+    for (int i = t; i < total; i += 256) {
+      const int r = i / groups;
+      const int gi = i - r * groups;
+      const uint32_t* p =
+          (const uint32_t*)(frame + (size_t)(y0 + r) * pitch + (size_t)(x0 + gi * 4) * 3);
+      const uint32_t w0 = p[0], w1 = p[1], w2 = p[2];
+      // bytes little-endian: w0 = b0 g0 r0 b1 | w1 = g1 r1 b2 g2 | w2 = r2 b3 g3 r3
+      const int y_0 = bgr_to_y(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255);
+      const int y_1 = bgr_to_y(w0 >> 24, w1 & 255, (w1 >> 8) & 255);
+      const int y_2 = bgr_to_y((w1 >> 16) & 255, w1 >> 24, w2 & 255);
+      const int y_3 = bgr_to_y((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24);
+      atomicAdd(&h[y_0], 1);
+      atomicAdd(&h[y_1], 1);
+      atomicAdd(&h[y_2], 1);
+      atomicAdd(&h[y_3], 1);
+    }
+  } else {
+    const int total = g.tw * g.th;
+    for (int i = t; i < total; i += 256) {
+      const int r = i / g.tw;
+      const int c = i - r * g.tw;
+      int sy = y0 + r;
+      if (sy >= H) sy = reflect101(sy, H);
+      int sx = x0 + c;
+      if (sx >= W) sx = reflect101(sx, W);
+      const uint8_t* p = frame + (size_t)sy * pitch + (size_t)sx * 3;
+      atomicAdd(&h[bgr_to_y(p[0], p[1], p[2])], 1);
+    }
+  }
+  __syncthreads();
+
+  int v = hist[0][t] + hist[1][t] + hist[2][t] + hist[3][t];
+  if (g.clip_limit > 0) {
+    int ex = v > g.clip_limit ? v - g.clip_limit : 0;
+    v = v > g.clip_limit ? g.clip_limit : v;
+    // block sum of the clipped excess
+    for (int off = 32; off > 0; off >>= 1) ex += __shfl_xor(ex, off);
+    if ((t & 63) == 0) wsum[wave] = ex;
+    __syncthreads();
+    const int clipped = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    const int batch = clipped / 256;
+    const int residual = clipped - batch * 256;
+    v += batch;
+    if (residual != 0) {
+      int step = 256 / residual;
+      if (step < 1) step = 1;
+      if (t % step == 0 && t / step < residual) v += 1;
+    }
+  }
+  // inclusive prefix sum over the 256 bins (Hillis-Steele in LDS)
+  scan[t] = v;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    int add = t >= off ? scan[t - off] : 0;
+    __syncthreads();
+    scan[t] += add;
+    __syncthreads();
+  }
+  const float f = (float)scan[t] * g.lut_scale;
+  lut[((size_t)b * g.tiles * g.tiles + tile) * 256 + t] = (uint8_t)sat_u8(__float2int_rn(f));
+}
+
+// CLAHE_Interpolation_Body per-axis coefficients.
+struct Interp {
+  int i1, i2;   // clamped tile indices
+  float a, a1;  // weight of i2 / of i1
+};
+__device__ __forceinline__ Interp interp_axis(int p, float inv, int tiles) {
+  Interp r;
+  const float f = (float)p * inv - 0.5f;
+  const int i1 = (int)floorf(f);
+  r.a = f - (float)i1;
+  r.a1 = 1.0f - r.a;
+  r.i1 = i1 < 0 ? 0 : i1;
+  r.i2 = (i1 + 1) > tiles - 1 ? tiles - 1 : i1 + 1;
+  return r;
+}
+
+// res = (L11*xa1 + L12*xa)*ya1 + (L21*xa1 + L22*xa)*ya, then cvRound+saturate.
+__device__ __forceinline__ int clahe_blend(int l11, int l12, int l21, int l22, const Interp& ix,
+                                           const Interp& iy) {
+  const float res = ((float)l11 * ix.a1 + (float)l12 * ix.a) * iy.a1 +
+                    ((float)l21 * ix.a1 + (float)l22 * ix.a) * iy.a;
+  return sat_u8(__float2int_rn(res));
+}
+
+// ---------------------------------------------------------------------------
+// Kernel B (standalone CLAHEDehaze): per pixel YCrCb, blend of the 4 tile
+// LUTs (read through L2), YCrCb->BGR.  One workgroup per 8-row strip.
+// ---------------------------------------------------------------------------
+constexpr int kApplyRows = 8;
+
+__global__ __launch_bounds__(256) void clahe_apply_kernel(const uint8_t* __restrict__ in,
+                                                          uint8_t* __restrict__ out,
+                                                          const uint8_t* __restrict__ lut, int H,
+                                                          int W, int pitch, ClaheGeo g) {
+  const int b = blockIdx.z;
+  const uint8_t* fin = in + (size_t)b * H * pitch;
+  uint8_t* fout = out + (size_t)b * H * pitch;
+  const uint8_t* flut = lut + (size_t)b * g.tiles * g.tiles * 256;
+  const int yb = blockIdx.y * kApplyRows;
+  const int ye = min(H, yb + kApplyRows);
+  for (int y = yb; y < ye; ++y) {
+    const Interp iy = interp_axis(y, g.inv_th, g.tiles);
+    const uint8_t* r1 = flut + (size_t)iy.i1 * g.tiles * 256;
+    const uint8_t* r2 = flut + (size_t)iy.i2 * g.tiles * 256;
+    const uint8_t* src = fin + (size_t)y * pitch;
+    uint8_t* dst = fout + (size_t)y * pitch;
+    for (int x = threadIdx.x; x < W; x += 256) {
+      const Interp ix = interp_axis(x, g.inv_tw, g.tiles);
+      int Y, Cr, Cb;
+      bgr_to_ycrcb(src[3 * x], src[3 * x + 1], src[3 * x + 2], Y, Cr, Cb);
+      const int y2 = clahe_blend(r1[ix.i1 * 256 + Y], r1[ix.i2 * 256 + Y], r2[ix.i1 * 256 + Y],
+                                 r2[ix.i2 * 256 + Y], ix, iy);
+      int bb, gg, rr;
+      ycrcb_to_bgr(y2, Cr, Cb, bb, gg, rr);
+      dst[3 * x] = (uint8_t)bb;
+      dst[3 * x + 1] = (uint8_t)gg;
+      dst[3 * x + 2] = (uint8_t)rr;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Median (+ optional fused CLAHE) on an LDS tile with halo.
+// Block = 256 threads -> BW x BH = 128 x 16 output pixels; each thread owns
+// two horizontal runs of 4 pixels (12 contiguous output bytes each).
+// Stage 1: raw rows (+halo, clamped) HBM -> LDS with 16-byte loads.
+// Stage 2: (optional CLAHE + colour round trip) raw -> processed tile,
+//          replicate-clamped columns.
+// Stage 3: median from the processed tile -> HBM.
+// ---------------------------------------------------------------------------
+constexpr int kBW = 128, kBH = 16;
+constexpr int kLutWinMax = 48;  // LUT tiles resident in LDS (12 KB)
+
+template <int K>
+struct MedTile {
+  static constexpr int R = K / 2;
+  static constexpr int TW = kBW + 2 * R;  // halo tile width (px)
+  static constexpr int TH = kBH + 2 * R;
+  static constexpr int RAWP = ((TW * 3 + 15 + 15) / 16) * 16 + 16;  // raw row stride (bytes)
+  static constexpr int PROC = TW * 3;                                // processed row stride
+};
+
+__device__ __forceinline__ uint8_t med3u(int a, int b, int c) {
+  return (uint8_t)max(min(a, b), min(max(a, b), c));
+}
+
+// 3x3: sort each column (lo, mid, hi) once, then
+// median = med3(max3(lo), med3(mid), min3(hi))  (exact for 9 samples).
+__device__ __forceinline__ void median3_run4(const uint8_t* __restrict__ tile, int stride, int hx,
+                                             int hy, uint8_t* __restrict__ o) {
+  // columns hx-1 .. hx+4 (tile coords already include the +R halo offset)
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    int lo[6], mi[6], hi[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int col = (hx - 1 + j) * 3 + c;
+      const int a = tile[(hy - 1) * stride + col];
+      const int b = tile[hy * stride + col];
+      const int d = tile[(hy + 1) * stride + col];
+      lo[j] = min(min(a, b), d);
+      hi[j] = max(max(a, b), d);
+      mi[j] = max(min(a, b), min(max(a, b), d));
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int l = max(max(lo[p], lo[p + 1]), lo[p + 2]);
+      const int m = med3u(mi[p], mi[p + 1], mi[p + 2]);
+      const int h = min(min(hi[p], hi[p + 1]), hi[p + 2]);
+      o[p * 3 + c] = med3u(l, m, h);
+    }
+  }
+}
+
+// Generic odd K: radix select of rank K*K/2 over the window held in VGPRs.
+template <int K>
+__device__ __forceinline__ uint8_t median_radix(const uint8_t* __restrict__ tile, int stride,
+                                                int hx, int hy, int c) {
+  constexpr int N = K * K;
+  constexpr int RANK = N / 2;
+  int w[N];
+#pragma unroll
+  for (int dy = 0; dy < K; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < K; ++dx)
+      w[dy * K + dx] = tile[(hy - K / 2 + dy) * stride + (hx - K / 2 + dx) * 3 + c];
+  int res = 0;
+#pragma unroll
+  for (int bit = 7; bit >= 0; --bit) {
+    const int cand = res | (1 << bit);
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) cnt += w[i] < cand ? 1 : 0;
+    if (cnt <= RANK) res = cand;
+  }
+  return (uint8_t)res;
+}
+
+template <int K, bool CLAHE>
+__global__ __launch_bounds__(256) void median_tile_kernel(const uint8_t* __restrict__ in,
+                                                          uint8_t* __restrict__ out,
+                                                          const uint8_t* __restrict__ lut, int H,
+                                                          int W, int pitch, ClaheGeo g) {
+  using T = MedTile<K>;
+  constexpr int R = T::R;
+  __shared__ __attribute__((aligned(16))) uint8_t raw[T::TH * T::RAWP];
+  __shared__ __attribute__((aligned(16))) uint8_t proc[T::TH * T::PROC + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t lwin[CLAHE ? kLutWinMax * 256 : 16];
+
+  const int tid = threadIdx.x;
+  const int b = blockIdx.z;
+  const int x0 = blockIdx.x * kBW, y0 = blockIdx.y * kBH;
+  const uint8_t* frame = in + (size_t)b * H * pitch;
+  const int rowbytes = W * 3;
+
+  // global byte window of the clamped halo columns
+  const int gx_lo = max(x0 - R, 0), gx_hi = min(x0 + kBW + R, W);  // [lo, hi)
+  const int bx0 = gx_lo * 3, bx1 = gx_hi * 3;
+  const int base = bx0 & ~15;
+  const int nch = ((bx1 + 15) & ~15) / 16 - base / 16;
+
+  // Stage 1: raw rows -> LDS
+  for (int i = tid; i < T::TH * nch; i += 256) {
+    const int hr = i / nch;
+    const int ch = i - hr * nch;
+    const int gy = min(max(y0 - R + hr, 0), H - 1);
+    const uint8_t* row = frame + (size_t)gy * pitch;
+    const int o = base + ch * 16;
+    uint8_t* dst = raw + hr * T::RAWP + ch * 16;
+    const uint8_t* src = row + o;
+    if (o + 16 <= rowbytes && (((uintptr_t)src) & 15) == 0) {
+      *(uint4*)dst = *(const uint4*)src;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (o + j < rowbytes) dst[j] = src[j];
+    }
+  }
+
+  // LUT window for the halo region (CLAHE only)
+  int wtx0 = 0, wty0 = 0, wtw = 0;
+  Interp iy_rows[1];
+  (void)iy_rows;
+  if constexpr (CLAHE) {
+    const uint8_t* flut = lut + (size_t)b * g.tiles * g.tiles * 256;
+    const int gy_lo = max(y0 - R, 0), gy_hi = min(y0 + kBH + R, H) - 1;
+    wtx0 = interp_axis(gx_lo, g.inv_tw, g.tiles).i1;
+    const int wtx1 = interp_axis(gx_hi - 1, g.inv_tw, g.tiles).i2;
+    wty0 = interp_axis(gy_lo, g.inv_th, g.tiles).i1;
+    const int wty1 = interp_axis(gy_hi, g.inv_th, g.tiles).i2;
+    wtw = wtx1 - wtx0 + 1;
+    const int wth = wty1 - wty0 + 1;
+    // host guarantees wtw*wth <= kLutWinMax
+    for (int i = tid; i < wtw * wth * 16; i += 256) {
+      const int tt = i >> 4, q = i & 15;
+      const int r = tt / wtw, c = tt - r * wtw;
+      const uint4* s = (const uint4*)(flut + ((size_t)(wty0 + r) * g.tiles + (wtx0 + c)) * 256);
+      ((uint4*)lwin)[i] = s[q];
+    }
+  }
+  __syncthreads();
+
+  // Stage 2: processed tile (clamped columns), optional CLAHE
+  for (int i = tid; i < T::TH * T::TW; i += 256) {
+    const int hr = i / T::TW;
+    const int hc = i - hr * T::TW;
+    const int gx = min(max(x0 - R + hc, 0), W - 1);
+    const uint8_t* p = raw + hr * T::RAWP + (gx * 3 - base);
+    int bb = p[0], gg = p[1], rr = p[2];
+    if constexpr (CLAHE) {
+      const int gy = min(max(y0 - R + hr, 0), H - 1);
+      const Interp ix = interp_axis(gx, g.inv_tw, g.tiles);
+      const Interp iy = interp_axis(gy, g.inv_th, g.tiles);
+      int Y, Cr, Cb;
+      bgr_to_ycrcb(bb, gg, rr, Y, Cr, Cb);
+      const uint8_t* l1 = lwin + (iy.i1 - wty0) * wtw * 256;
+      const uint8_t* l2 = lwin + (iy.i2 - wty0) * wtw * 256;
+      const int c1 = (ix.i1 - wtx0) * 256 + Y, c2 = (ix.i2 - wtx0) * 256 + Y;
+      const int y2 = clahe_blend(l1[c1], l1[c2], l2[c1], l2[c2], ix, iy);
+      ycrcb_to_bgr(y2, Cr, Cb, bb, gg, rr);
+    }
+    uint8_t* q = proc + hr * T::PROC + hc * 3;
+    q[0] = (uint8_t)bb;
+    q[1] = (uint8_t)gg;
+    q[2] = (uint8_t)rr;
+  }
+  __syncthreads();
+
+  // Stage 3: medians, 2 runs of 4 px per thread
+  uint8_t* fout = out + (size_t)b * H * pitch;
+#pragma unroll
+  for (int run = 0; run < 2; ++run) {
+    const int idx = tid + run * 256;     // 0..511
+    const int ry = idx >> 5;             // 0..15
+    const int rx = (idx & 31) * 4;       // 0..124
+    const int y = y0 + ry, x = x0 + rx;
+    if (y >= H || x >= W) continue;
+    uint8_t o[12];
+    if constexpr (K == 3) {
+      median3_run4(proc, T::PROC, rx + R, ry + R, o);
+    } else {
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o[p * 3 + c] = median_radix<K>(proc, T::PROC, rx + p + R, ry + R, c);
+    }
+    uint8_t* dst = fout + (size_t)y * pitch + (size_t)x * 3;
+    const int n = min(4, W - x) * 3;
+    if (n == 12 && (((uintptr_t)dst) & 3) == 0) {
+      uint32_t w0 = o[0] | (o[1] << 8) | (o[2] << 16) | ((uint32_t)o[3] << 24);
+      uint32_t w1 = o[4] | (o[5] << 8) | (o[6] << 16) | ((uint32_t)o[7] << 24);
+      uint32_t w2 = o[8] | (o[9] << 8) | (o[10] << 16) | ((uint32_t)o[11] << 24);
+      ((uint32_t*)dst)[0] = w0;
+      ((uint32_t*)dst)[1] = w1;
+      ((uint32_t*)dst)[2] = w2;
+    } else {
+      for (int j = 0; j < n; ++j) dst[j] = o[j];
+    }
+  }
+}
+
+// Gray span for the low-contrast gate (pipeline.py:24-30).
+__global__ __launch_bounds__(256) void gray_span_kernel(const uint8_t* __restrict__ in, int H,
+                                                        int W, int pitch, int* __restrict__ mn_mx) {
+  const int b = blockIdx.y;
+  const uint8_t* frame = in + (size_t)b * H * pitch;
+  int mn = 255, mx = 0;
+  const int total = H * W;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int y = i / W, x = i - (i / W) * W;
+    const uint8_t* p = frame + (size_t)y * pitch + (size_t)x * 3;
+    const int v = bgr_to_y(p[0], p[1], p[2]);
+    mn = min(mn, v);
+    mx = max(mx, v);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    mn = min(mn, __shfl_xor(mn, off));
+    mx = max(mx, __shfl_xor(mx, off));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&mn_mx[2 * b], mn);
+    atomicMax(&mn_mx[2 * b + 1], mx);
+  }
+}
+__global__ void gray_span_init(int* mn_mx, int B) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) {
+    mn_mx[2 * i] = 255;
+    mn_mx[2 * i + 1] = 0;
+  }
+}
+__global__ void gray_span_finish(const int* mn_mx, int* span, int B) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) span[i] = mn_mx[2 * i + 1] - mn_mx[2 * i];
+}
+
+static bool lut_window_fits(const ClaheGeo& g, int K) {
+  const int R = K / 2;
+  // worst-case tile columns/rows touched by one (kBW+2R) x (kBH+2R) halo tile
+  const int cols = (kBW + 2 * R - 1) / g.tw + 3;
+  const int rows = (kBH + 2 * R - 1) / g.th + 3;
+  return min(cols, g.tiles) * min(rows, g.tiles) <= kLutWinMax;
+}
+
+template <int K, bool CLAHE>
+static void launch_median(const uint8_t* in, uint8_t* out, const uint8_t* lut, int B, int H,
+                          int W, int pitch, const ClaheGeo& g, hipStream_t s) {
+  dim3 grid(ceil_div(W, kBW), ceil_div(H, kBH), B);
+  median_tile_kernel<K, CLAHE><<<grid, 256, 0, s>>>(in, out, lut, H, W, pitch, g);
+}
+
+template <bool CLAHE>
+static void dispatch_median(int k, const uint8_t* in, uint8_t* out, const uint8_t* lut, int B,
+                            int H, int W, int pitch, const ClaheGeo& g, hipStream_t s) {
+  switch (k) {
+    case 3: launch_median<3, CLAHE>(in, out, lut, B, H, W, pitch, g, s); break;
+    case 5: launch_median<5, CLAHE>(in, out, lut, B, H, W, pitch, g, s); break;
+    case 7: launch_median<7, CLAHE>(in, out, lut, B, H, W, pitch, g, s); break;
+    default: launch_median<9, CLAHE>(in, out, lut, B, H, W, pitch, g, s); break;
+  }
+}
+
+}  // namespace rv
+
+using namespace rv;
+
+static int check_frames(const uint8_t* in, const void* out, int B, int H, int W, int pitch) {
+  RV_CHECK_ARG(in != nullptr && out != nullptr, "null frame pointer");
+  RV_CHECK_ARG(B >= 0 && H > 0 && W > 0, "bad frame shape B=%d H=%d W=%d", B, H, W);
+  RV_CHECK_ARG(pitch >= 3 * W, "pitch %d < 3*W", pitch);
+  RV_CHECK_ARG((const void*)in != out, "in and out must not alias");
+  return RV_OK;
+}
+
+extern "C" size_t rv_clahe_ws_bytes(int B, int tiles) {
+  if (B <= 0 || tiles <= 0) return 0;
+  return (size_t)B * tiles * tiles * 256;
+}
+
+extern "C" int rv_clahe_ycrcb_u8(const uint8_t* in, uint8_t* out, int B, int H, int W, int pitch,
+                                 int tiles, double clip, void* ws, size_t ws_bytes, void* stream) {
+  int st = check_frames(in, out, B, H, W, pitch);
+  if (st) return st;
+  RV_CHECK_ARG(tiles >= 1 && tiles <= 64, "tiles %d out of range", tiles);
+  RV_CHECK_ARG(ws != nullptr && ws_bytes >= rv_clahe_ws_bytes(B, tiles), "workspace too small");
+  if (B == 0) return RV_OK;
+  ClaheGeo g = make_geo(H, W, tiles, clip);
+  hipStream_t s = as_stream(stream);
+  uint8_t* lut = (uint8_t*)ws;
+  clahe_lut_kernel<<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  clahe_apply_kernel<<<dim3(1, ceil_div(H, kApplyRows), B), 256, 0, s>>>(in, out, lut, H, W,
+                                                                          pitch, g);
+  return launch_status("rv_clahe_ycrcb_u8");
+}
+
+extern "C" int rv_median_u8c3(const uint8_t* in, uint8_t* out, int B, int H, int W, int pitch,
+                              int k, void* stream) {
+  int st = check_frames(in, out, B, H, W, pitch);
+  if (st) return st;
+  RV_CHECK_ARG(k == 3 || k == 5 || k == 7 || k == 9, "median k=%d must be 3,5,7,9", k);
+  if (B == 0) return RV_OK;
+  ClaheGeo g{};
+  dispatch_median<false>(k, in, out, nullptr, B, H, W, pitch, g, as_stream(stream));
+  return launch_status("rv_median_u8c3");
+}
+
+extern "C" int rv_clahe_median_u8(const uint8_t* in, uint8_t* out, int B, int H, int W, int pitch,
+                                  int tiles, double clip, int k, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  int st = check_frames(in, out, B, H, W, pitch);
+  if (st) return st;
+  RV_CHECK_ARG(tiles >= 1 && tiles <= 64, "tiles %d out of range", tiles);
+  RV_CHECK_ARG(k == 3 || k == 5 || k == 7 || k == 9, "median k=%d must be 3,5,7,9", k);
+  RV_CHECK_ARG(ws != nullptr && ws_bytes >= rv_clahe_ws_bytes(B, tiles), "workspace too small");
+  if (B == 0) return RV_OK;
+  ClaheGeo g = make_geo(H, W, tiles, clip);
+  hipStream_t s = as_stream(stream);
+  uint8_t* lut = (uint8_t*)ws;
+  RV_CHECK_ARG(lut_window_fits(g, k),
+               "LUT window too large for the fused pass (tiles=%d, tile %dx%d); "
+               "use rv_clahe_ycrcb_u8 + rv_median_u8c3",
+               tiles, g.tw, g.th);
+  clahe_lut_kernel<<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  dispatch_median<true>(k, in, out, lut, B, H, W, pitch, g, s);
+  return launch_status("rv_clahe_median_u8");
+}
+
+extern "C" int rv_clahe_median_fits(int H, int W, int tiles, int k) {
+  if (H <= 0 || W <= 0 || tiles < 1 || tiles > 64) return 0;
+  return lut_window_fits(make_geo(H, W, tiles, 0.0), k) ? 1 : 0;
+}
+
+extern "C" int rv_gray_span_u8(const uint8_t* in, int B, int H, int W, int pitch, int* ws,
+                               int* span_out, void* stream) {
+  RV_CHECK_ARG(in != nullptr && ws != nullptr && span_out != nullptr, "null pointer");
+  RV_CHECK_ARG(B >= 0 && H > 0 && W > 0 && pitch >= 3 * W, "bad frame shape");
+  if (B == 0) return RV_OK;
+  hipStream_t s = as_stream(stream);
+  gray_span_init<<<ceil_div(B, 256), 256, 0, s>>>(ws, B);
+  const int blocks = min(256, ceil_div(H * W, 256));
+  gray_span_kernel<<<dim3(blocks, B), 256, 0, s>>>(in, H, W, pitch, ws);
+  gray_span_finish<<<ceil_div(B, 256), 256, 0, s>>>(ws, span_out, B);
+  return launch_status("rv_gray_span_u8");
+}

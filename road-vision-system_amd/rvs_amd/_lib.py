@@ -1,0 +1,106 @@
+"""ctypes binding of librvhip.so (the C ABI declared in include/rvhip.h).
+
+The product path has exactly one implementation: the gfx950 HIP kernels in
+this library.  If the library is missing or cannot be loaded, every op raises
+immediately -- there is deliberately no CPU fallback (the reference's
+``ops_cuda`` soft-fallback, src/preprocess/ops_cuda/cuda_clahe_dehaze.py:22-39,
+is replaced by a loud failure so a silent slow path can never be measured).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_double, c_float, c_int, c_size_t, c_void_p, POINTER
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librvhip.so")
+
+_lib = None
+
+
+class RVError(RuntimeError):
+    """A non-zero status returned through the C ABI."""
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "rv_abi_version": (c_int, []),
+    "rv_last_error": (ctypes.c_char_p, []),
+    "rv_clahe_ws_bytes": (c_size_t, [c_int, c_int]),
+    "rv_clahe_ycrcb_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                  c_double, c_void_p, c_size_t, c_void_p]),
+    "rv_median_u8c3": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "rv_clahe_median_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                   c_double, c_int, c_void_p, c_size_t, c_void_p]),
+    "rv_clahe_median_fits": (c_int, [c_int, c_int, c_int, c_int]),
+    "rv_gray_span_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                c_void_p]),
+    "rv_letterbox_geometry": (c_int, [c_int, c_int, c_int, c_int, POINTER(c_int)]),
+    "rv_letterbox_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                POINTER(c_int), c_void_p]),
+}
+
+
+def load():
+    """Load librvhip.so once; raise if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RVError(
+            f"{LIB_PATH} not found: build it with `make -C road-vision-system_amd/csrc` "
+            "or __graft_entry__.build(); the HIP path has no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def register(name, restype, argtypes):
+    """Declare an additional ABI entry (used by modules as they grow)."""
+    _SIGS[name] = (restype, argtypes)
+    if _lib is not None:
+        fn = getattr(_lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+
+
+def check(status: int, what: str = "") -> None:
+    if status != 0:
+        msg = load().rv_last_error().decode(errors="replace")
+        raise RVError(f"{what or 'rvhip'} failed with status {status}: {msg}")
+
+
+_NOCHECK = {"rv_abi_version", "rv_clahe_median_fits"}
+
+
+def call(name: str, *args) -> int:
+    fn = getattr(load(), name)
+    st = fn(*args)
+    if fn.restype is c_int and name not in _NOCHECK:
+        check(st, name)
+    return st
+
+
+def stream_ptr(stream=None) -> int:
+    """hipStream_t of a torch stream (default: current stream) as an int."""
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def ptr(t) -> int:
+    """Device pointer of a torch tensor (None -> 0)."""
+    return 0 if t is None else int(t.data_ptr())
+
+
+def int_array(vals):
+    arr = (c_int * len(vals))(*[int(v) for v in vals])
+    return arr
+
+
+__all__ = ["load", "check", "call", "stream_ptr", "ptr", "int_array", "register", "RVError",
+           "LIB_PATH", "c_int", "c_float", "c_double", "c_size_t", "c_void_p", "POINTER"]

@@ -1,0 +1,104 @@
+"""Functional torch-tensor front end over the C ABI (include/rvhip.h).
+
+Every function takes device-resident uint8 BGR frames shaped (B, H, W, 3)
+(or (H, W, 3)), launches on the current torch stream and returns device
+tensors.  Nothing here copies to the host or synchronises.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr
+
+
+def _frames(x: torch.Tensor) -> Tuple[torch.Tensor, int, int, int, int]:
+    if x.dim() == 3:
+        x = x.unsqueeze(0)
+    if x.dim() != 4 or x.shape[-1] != 3 or x.dtype != torch.uint8:
+        raise ValueError(f"expected uint8 frames (B,H,W,3), got {tuple(x.shape)} {x.dtype}")
+    if not x.is_cuda:
+        raise ValueError("frames must be on the GPU (HIP path has no CPU fallback)")
+    B, H, W, _ = x.shape
+    if not (x.stride(3) == 1 and x.stride(2) == 3 and x.stride(0) == H * x.stride(1)):
+        x = x.contiguous()
+    pitch = x.stride(1)
+    return x, B, H, W, pitch
+
+
+def _like(x: torch.Tensor, out: Optional[torch.Tensor]) -> torch.Tensor:
+    """Output frames with the same (B, H, pitch) layout as the input: the ABI
+    takes one pitch for both."""
+    if out is None:
+        return torch.empty_strided(x.shape, x.stride(), dtype=x.dtype, device=x.device)
+    if out.shape != x.shape or out.stride() != x.stride():
+        raise ValueError("out must have the input's shape and strides")
+    return out
+
+
+def clahe_ws_bytes(B: int, tiles: int) -> int:
+    return int(_lib.load().rv_clahe_ws_bytes(B, tiles))
+
+
+def _ws(B, tiles, ws, device):
+    need = clahe_ws_bytes(B, tiles)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(max(need, 1), dtype=torch.uint8, device=device)
+    return ws, need
+
+
+def clahe_ycrcb(frames: torch.Tensor, tiles: int = 8, clip: float = 2.0,
+                out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None):
+    x, B, H, W, pitch = _frames(frames)
+    out = _like(x, out)
+    ws, need = _ws(B, tiles, ws, x.device)
+    call("rv_clahe_ycrcb_u8", ptr(x), ptr(out), B, H, W, pitch, int(tiles), float(clip),
+         ptr(ws), ws.numel(), stream_ptr())
+    return out if frames.dim() == 4 else out[0]
+
+
+def median(frames: torch.Tensor, k: int = 3, out: Optional[torch.Tensor] = None):
+    x, B, H, W, pitch = _frames(frames)
+    out = _like(x, out)
+    call("rv_median_u8c3", ptr(x), ptr(out), B, H, W, pitch, int(k), stream_ptr())
+    return out if frames.dim() == 4 else out[0]
+
+
+def clahe_median(frames: torch.Tensor, tiles: int = 8, clip: float = 2.0, k: int = 3,
+                 out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None):
+    x, B, H, W, pitch = _frames(frames)
+    out = _like(x, out)
+    ws, need = _ws(B, tiles, ws, x.device)
+    call("rv_clahe_median_u8", ptr(x), ptr(out), B, H, W, pitch, int(tiles), float(clip),
+         int(k), ptr(ws), ws.numel(), stream_ptr())
+    return out if frames.dim() == 4 else out[0]
+
+
+def clahe_median_fits(frames: torch.Tensor, tiles: int, k: int) -> bool:
+    H, W = frames.shape[-3], frames.shape[-2]
+    return bool(_lib.load().rv_clahe_median_fits(H, W, int(tiles), int(k)))
+
+
+def gray_span(frames: torch.Tensor) -> torch.Tensor:
+    x, B, H, W, pitch = _frames(frames)
+    ws = torch.empty(2 * B, dtype=torch.int32, device=x.device)
+    span = torch.empty(B, dtype=torch.int32, device=x.device)
+    call("rv_gray_span_u8", ptr(x), B, H, W, pitch, ptr(ws), ptr(span), stream_ptr())
+    return span
+
+
+def letterbox_geometry(H: int, W: int, imgsz: int = 640, stride: int = 32):
+    geo = _lib.int_array([0] * 6)
+    call("rv_letterbox_geometry", H, W, imgsz, stride, geo)
+    return tuple(int(v) for v in geo)
+
+
+def letterbox(frames: torch.Tensor, geo, out: Optional[torch.Tensor] = None):
+    x, B, H, W, pitch = _frames(frames)
+    oh, ow = geo[0], geo[1]
+    if out is None:
+        out = torch.empty((B, oh, ow, 3), dtype=torch.uint8, device=x.device)
+    call("rv_letterbox_u8", ptr(x), ptr(out), B, H, W, pitch, _lib.int_array(geo), stream_ptr())
+    return out
