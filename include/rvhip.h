@@ -97,6 +97,81 @@ int rv_letterbox_geometry(int H, int W, int imgsz, int stride, int* geo);
 int rv_letterbox_u8(const uint8_t* in, uint8_t* out, int B, int H, int W,
                     int pitch, const int* geo, void* stream);
 
+
+/* --- YOLOv8 model (the Ultralytics graph run by model.predict,
+ * yolo_ultralytics.py:16-35).  variant: 0=n 1=s 2=m 3=l 4=x (yolov8.yaml
+ * scales).  Weights are BN-fused conv weights + biases in Ultralytics
+ * state_dict order (rv_yolo_conv_info), flattened as, per conv,
+ * weight[cout][cin][k][k] then bias[cout] (f32). */
+int rv_yolo_num_convs(int variant);
+/* info[5] = {cin, cout, k, stride, silu}; name = "model.2.m.0.cv1" etc. */
+int rv_yolo_conv_info(int variant, int idx, int* info, char* name, int name_cap);
+size_t rv_yolo_flat_floats(int variant);
+size_t rv_yolo_packed_bytes(int variant);
+/* Host-side packer: flat f32 -> device layout (bf16 [Cout16][ky][kx][Cin32],
+ * f32 biases); the caller copies host_out to device memory it owns. */
+int rv_yolo_pack(int variant, const float* flat, size_t n, void* host_out, size_t out_bytes);
+/* Plan a model for in_h x in_w letterboxed inputs (multiples of 32) and up
+ * to max_B images; dev_packed must stay valid for the handle's lifetime. */
+int rv_yolo_create(int variant, const void* dev_packed, int max_B, int in_h, int in_w,
+                   void** handle);
+int rv_yolo_destroy(void* handle);
+size_t rv_yolo_ws_bytes(void* handle, int B);
+int rv_yolo_num_anchors(void* handle);
+/* Forward on B letterboxed u8 BGR images (B x in_h x in_w x 3).  raw_out
+ * (nullable): the reference's raw prediction (B, 4+nc, A) f32 = cat(xywh *
+ * stride, sigmoid(cls)).  cand (nullable): per image up to cand_cap NMS
+ * candidate rows {x1,y1,x2,y2,score,cls,anchor,pad} (32 B) whose best class
+ * score > conf, count in cand_n[B] (zeroed by this call). */
+int rv_yolo_forward(void* handle, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
+                    float* raw_out, float conf, void* cand, int cand_cap, int* cand_n,
+                    void* stream);
+
+/* Introspection for layer-wise parity tests: activation buffers (NHWC,
+ * info = {H, W, C, is_f32}, byte offset inside the workspace for batch B)
+ * and the conv launches of the last forward (20 ints each: conv index,
+ * input view {buf, cs, co, Hin, Win}, Ho, Wo, two output views {buf, cs, co,
+ * upsample}, residual view {buf, cs, co}, pad).  Returns the record count. */
+int rv_yolo_num_buffers(void* handle);
+int rv_yolo_buffer_info(void* handle, int B, int buf, int* info, size_t* off_bytes);
+int rv_yolo_trace(void* handle, int* recs, int max_recs);
+
+/* --- Ultralytics non_max_suppression + scale_boxes + class filter
+ * (yolo_ultralytics.py:28-53), one workgroup per image. */
+size_t rv_nms_smem_bytes(void);
+/* scale5 = {gain (f32 of the python gain), pad_x, pad_y, clip_w, clip_h};
+ * keep_mask4 (nullable = keep all): 128-bit class mask (classes_keep);
+ * out: B x max_det x 6 {x1,y1,x2,y2,conf,cls} in score order, out_n[B]. */
+int rv_nms_postprocess(const void* cand, const int* cand_n, int B, int cap, float iou,
+                       int max_det, float max_wh, const float* scale5,
+                       const uint32_t* keep_mask4, float* out, int* out_n, void* stream);
+/* Candidate rows from a reference-layout raw prediction (B, 4+nc, A). */
+int rv_candidates_from_raw(const float* raw, int B, int nc, int A, float conf, void* cand,
+                           int cap, int* cand_n, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Track: SortTracker.update (src/track/sort_tracker.py:212-278) batched over */
+/* S independent streams, with GroundProjector metrics (projector.py:13-84). */
+/* ------------------------------------------------------------------------ */
+size_t rv_sort_state_bytes(int S, int tmax);
+size_t rv_sort_ws_bytes(int S, int tmax, int dmax);
+/* Zero the state (no tracks, next_id = 1); synchronises `stream`. */
+int rv_sort_init(void* state, int S, int tmax, void* stream);
+/* One frame per stream.  state_in is consumed (used as the work copy);
+ * state_out receives the new state (ping-pong).  dets: S x dmax x 6
+ * {x1,y1,x2,y2,conf,cls} f32 (post class-filter), dcount[S]; ts[S] seconds.
+ * params6 = {max_staleness, min_hits, iou_threshold, speed_window,
+ * max_distance (<0 = None), 0}.  H9 (nullable = no projector): row-major
+ * f64 homography; origin2: projector origin (f32).  Outputs per detection
+ * (S x dmax): track id (-1 = None), distance_m and speed_kmh (NaN = None). */
+int rv_sort_update(void* state_in, void* state_out, int S, int tmax, const float* dets,
+                   const int* dcount, int dmax, const double* ts, const double* params6,
+                   const double* H9, const float* origin2, void* ws, size_t ws_bytes,
+                   int* out_id, double* out_dist, double* out_speed, void* stream);
+/* Debug/parity export: per track x[7] (f64) and {id, hits, hit_streak, cls}. */
+int rv_sort_export(const void* state, int S, int tmax, double* x_out, int* meta, int* T_out,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

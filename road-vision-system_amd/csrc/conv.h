@@ -1,0 +1,65 @@
+// Internal interface of the YOLOv8 conv / head kernels (conv.hip) used by the
+// model plan (yolo.hip).  Activations are NHWC bf16 (raw uint16 bits);
+// a "view" is (base pointer, channel stride of the buffer, channel offset),
+// so concatenation is free: producers write into a slice of a wider buffer
+// and consumers read a slice.
+#pragma once
+#include "common.h"
+
+namespace rv {
+
+typedef uint16_t bf16_t;
+
+struct ConvArgs {
+  // input view
+  const bf16_t* in;
+  int in_cs, in_co;
+  int Hin, Win, Cin;
+  // packed weights [Cout_pad16][k*k][Cin_pad32] bf16, bias [Cout_pad16] f32
+  const bf16_t* w;
+  const float* bias;
+  int Cout, k, stride, pad;
+  int Ho, Wo, B;
+  // up to two output views; up = 1 writes a nearest-2x upsampled copy
+  void* out0;
+  int out0_cs, out0_co, out0_up;
+  void* out1;
+  int out1_cs, out1_co, out1_up;
+  int out_f32;  // 1: outputs are f32 (detect logits), else bf16
+  // optional residual view (same spatial size as the output): v += res
+  const bf16_t* res;
+  int res_cs, res_co;
+  int act;  // 1: SiLU
+};
+
+// Implicit-GEMM conv on MFMA (v_mfma_f32_16x16x32_bf16).
+int launch_conv(const ConvArgs& a, hipStream_t s);
+
+// First conv (3 -> C0, k3 s2 p1) straight from the u8 BGR letterboxed
+// frame, f32 arithmetic: x = u8/255 with the RGB order of the reference
+// (predictor preprocess: im[..., ::-1] / 255).  w: [C0][3 rgb][3][3] f32.
+int launch_conv0(const uint8_t* img, int B, int H, int W, const float* w, const float* bias,
+                 int C0, bf16_t* out, int out_cs, hipStream_t s);
+
+// SPPF pooling: buf holds x in channels [0, c); writes maxpool5, maxpool5^2
+// and maxpool5^3 (= clipped 5/9/13 windows) into [c,2c), [2c,3c), [3c,4c).
+int launch_sppf_pool(bf16_t* buf, int B, int H, int W, int c, hipStream_t s);
+
+struct HeadLevel {
+  const float* logits;  // [B][H][W][cs] f32: [0,4*reg) box bins, [4*reg, 4*reg+nc) classes
+  int H, W, cs;
+  float stride;
+};
+
+struct Cand {  // one detection candidate (Ultralytics NMS row before NMS)
+  float x1, y1, x2, y2, score;
+  int cls, anchor, pad;
+};
+
+// DFL + dist2bbox + sigmoid for all anchors.  Optionally writes the
+// reference's raw output (B, 4+nc, A) and appends every anchor whose best
+// class score > conf to cand[b][*] (count in cand_n[b], zeroed by caller).
+int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_max, float conf,
+                         float* raw, Cand* cand, int cand_cap, int* cand_n, hipStream_t s);
+
+}  // namespace rv

@@ -1,0 +1,272 @@
+// Batched Ultralytics non_max_suppression + scale_boxes + class filter on
+// gfx950: one workgroup per image.
+//
+// Reference: src/detect/yolo_ultralytics.py:28-53 -> Ultralytics
+// non_max_suppression(conf, iou, max_det, max_nms=30000, max_wh=7680,
+// agnostic=False) -> torchvision.ops.nms (CPU kernel semantics: stable
+// descending score sort, greedy suppression of later boxes whose IoU with a
+// kept box is `> iou_threshold` compared in double, IoU on class-offset
+// f32 boxes) -> i[:max_det] -> scale_boxes (subtract pad, divide by gain,
+// clip) -> the reference's own post-NMS class filter (classes_keep,
+// yolo_ultralytics.py:49-50).
+//
+// Sort: 64-bit keys (~score_bits, anchor, slot) bitonic-sorted in LDS
+// (score desc, anchor asc == the stable order of rows in anchor order).
+// Greedy: wave 0 walks the sorted list in chunks of 64; each lane tests its
+// candidate against every kept box, builds the 64-bit mask of later chunk
+// members it would suppress, and a uniform scalar loop resolves the chunk.
+#include "conv.h"
+
+namespace rv {
+
+constexpr int kSortCap = 16384;  // candidates per image held in LDS (128 KB)
+constexpr int kMaxDet = 1024;
+
+struct ScaleArgs {
+  float gain;   // f32(gain) as torch divides by the python-float gain
+  float pad_x, pad_y;
+  float clip_w, clip_h;
+};
+
+// compiler-level ordering of LDS accesses between lanes of one wave (the
+// hardware executes a wave's LDS ops in order)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ float4 offset_box(const Cand& c, float max_wh) {
+  const float off = (float)c.cls * max_wh;
+  return make_float4(c.x1 + off, c.y1 + off, c.x2 + off, c.y2 + off);
+}
+
+// torchvision nms_kernel_impl IoU test: i kept (earlier), j later.
+__device__ __forceinline__ bool suppresses(float4 bi, float ai, float4 bj, float aj, double thr) {
+  const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
+  const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
+  const float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
+  const float inter = w * h;
+  const float ovr = inter / (ai + aj - inter);
+  return (double)ovr > thr;
+}
+
+__global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand,
+                                                   const int* __restrict__ cand_n, int cap,
+                                                   float max_wh, double iou, int max_det,
+                                                   ScaleArgs sc, const uint32_t* __restrict__ keep4,
+                                                   float* __restrict__ out, int* __restrict__ out_n) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint64_t* keys = (uint64_t*)smem;                       // kSortCap
+  float4* kbox = (float4*)(smem + kSortCap * 8);          // kept offset boxes (kMaxDet)
+  float* karea = (float*)(kbox + kMaxDet);                // kMaxDet
+  int* kslot = (int*)(karea + kMaxDet);                   // kMaxDet
+  float4* cbox = (float4*)(kslot + kMaxDet);              // chunk boxes (64)
+  float* carea = (float*)(cbox + 64);                     // 64
+  uint64_t* cmask = (uint64_t*)(carea + 64);              // 64
+  __shared__ int s_nkeep;
+
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const Cand* cb = cand + (size_t)b * cap;
+  int n = cand_n[b];
+  if (n > cap) n = cap;
+  if (n > kSortCap) n = kSortCap;  // capacity limit (documented in DESIGN.md)
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  for (int i = tid; i < np2; i += blockDim.x) {
+    uint64_t k = ~0ull;
+    if (i < n) {
+      const Cand c = cb[i];
+      const uint32_t sb = __float_as_uint(c.score);  // score > conf >= 0: bits are monotonic
+      k = ((uint64_t)(~sb) << 32) | ((uint64_t)(uint32_t)c.anchor << 16) | (uint64_t)i;
+    }
+    keys[i] = k;
+  }
+  __syncthreads();
+  // bitonic sort ascending
+  for (int size = 2; size <= np2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < np2 / 2; i += blockDim.x) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const uint64_t a = keys[lo], c = keys[hi];
+        if ((a > c) == up) {
+          keys[lo] = c;
+          keys[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // greedy NMS on wave 0
+  if (tid < 64) {
+    const int lane = tid;
+    int nkeep = 0;
+    for (int base = 0; base < n && nkeep < max_det; base += 64) {
+      const int i = base + lane;
+      const bool valid = i < n;
+      float4 bx = make_float4(0.f, 0.f, 0.f, 0.f);
+      float ar = 0.f;
+      int slot = 0;
+      if (valid) {
+        slot = (int)(keys[i] & 0xFFFF);
+        bx = offset_box(cb[slot], max_wh);
+        ar = (bx.z - bx.x) * (bx.w - bx.y);
+      }
+      bool sup = !valid;
+      for (int k = 0; k < nkeep && !sup; ++k) sup = suppresses(kbox[k], karea[k], bx, ar, iou);
+      cbox[lane] = bx;
+      carea[lane] = ar;
+      wave_sync();
+      uint64_t m = 0;
+      if (valid) {
+        for (int j = lane + 1; j < 64 && base + j < n; ++j)
+          if (suppresses(bx, ar, cbox[j], carea[j], iou)) m |= 1ull << j;
+      }
+      cmask[lane] = m;
+      wave_sync();
+      uint64_t alive = __ballot(!sup);
+      uint64_t kept = 0;
+      int room = max_det - nkeep;
+      for (int q = 0; q < 64 && room > 0; ++q) {
+        if ((alive >> q) & 1ull) {
+          kept |= 1ull << q;
+          alive &= ~cmask[q];
+          --room;
+        }
+      }
+      if ((kept >> lane) & 1ull) {
+        const int pos = nkeep + __popcll(kept & ((1ull << lane) - 1ull));
+        kbox[pos] = bx;
+        karea[pos] = ar;
+        kslot[pos] = slot;
+      }
+      nkeep += __popcll(kept);
+      wave_sync();
+    }
+    if (lane == 0) s_nkeep = nkeep;
+  }
+  __syncthreads();
+  // scale_boxes + clip + post-NMS class filter, order preserved
+  if (tid < 64) {
+    const int nkeep = s_nkeep;
+    int w = 0;
+    for (int base = 0; base < nkeep; base += 64) {
+      const int k = base + tid;
+      bool ok = false;
+      Cand c;
+      if (k < nkeep) {
+        c = cb[kslot[k]];
+        ok = keep4 == nullptr || ((keep4[(c.cls >> 5) & 3] >> (c.cls & 31)) & 1u);
+      }
+      const uint64_t bal = __ballot(ok);
+      if (ok) {
+        const int pos = w + __popcll(bal & ((1ull << tid) - 1ull));
+        float x1 = (c.x1 - sc.pad_x) / sc.gain, y1 = (c.y1 - sc.pad_y) / sc.gain;
+        float x2 = (c.x2 - sc.pad_x) / sc.gain, y2 = (c.y2 - sc.pad_y) / sc.gain;
+        x1 = fminf(fmaxf(x1, 0.f), sc.clip_w);
+        y1 = fminf(fmaxf(y1, 0.f), sc.clip_h);
+        x2 = fminf(fmaxf(x2, 0.f), sc.clip_w);
+        y2 = fminf(fmaxf(y2, 0.f), sc.clip_h);
+        float* o = out + ((size_t)b * max_det + pos) * 6;
+        o[0] = x1;
+        o[1] = y1;
+        o[2] = x2;
+        o[3] = y2;
+        o[4] = c.score;
+        o[5] = (float)c.cls;
+      }
+      w += __popcll(bal);
+    }
+    if (tid == 0) out_n[b] = w;
+  }
+}
+
+// Reference-layout candidates: raw (B, 4+nc, A) -> Cand rows (xc filter,
+// xywh2xyxy, best class), i.e. the first half of non_max_suppression.
+__global__ __launch_bounds__(256) void raw_candidates_kernel(const float* __restrict__ raw, int nc,
+                                                             int A, float conf,
+                                                             Cand* __restrict__ cand, int cap,
+                                                             int* __restrict__ cand_n) {
+  const int a = blockIdx.x * 256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (a >= A) return;
+  const float* r = raw + (size_t)b * (4 + nc) * A;
+  float best = -INFINITY;
+  int bc = 0;
+  for (int c = 0; c < nc; ++c) {
+    const float s = r[(size_t)(4 + c) * A + a];
+    if (s > best) {
+      best = s;
+      bc = c;
+    }
+  }
+  if (!(best > conf)) return;
+  const float cx = r[a], cy = r[(size_t)A + a], w = r[(size_t)2 * A + a], h = r[(size_t)3 * A + a];
+  const float hw = w / 2.0f, hh = h / 2.0f;
+  const int i = atomicAdd(&cand_n[b], 1);
+  if (i < cap) {
+    Cand c;
+    c.x1 = cx - hw;
+    c.y1 = cy - hh;
+    c.x2 = cx + hw;
+    c.y2 = cy + hh;
+    c.score = best;
+    c.cls = bc;
+    c.anchor = a;
+    c.pad = 0;
+    cand[(size_t)b * cap + i] = c;
+  }
+}
+
+}  // namespace rv
+
+using namespace rv;
+
+extern "C" size_t rv_nms_smem_bytes(void) {
+  return (size_t)kSortCap * 8 + (size_t)kMaxDet * (16 + 4 + 4) + 64 * (16 + 4 + 8);
+}
+
+extern "C" int rv_nms_postprocess(const void* cand, const int* cand_n, int B, int cap, float iou,
+                                  int max_det, float max_wh, const float* scale5,
+                                  const uint32_t* keep_mask4, float* out, int* out_n,
+                                  void* stream) {
+  RV_CHECK_ARG(cand && cand_n && out && out_n && scale5, "null pointer");
+  RV_CHECK_ARG(B >= 0 && cap > 0 && cap <= 65536, "cap %d outside (0, 65536]", cap);
+  RV_CHECK_ARG(max_det > 0 && max_det <= kMaxDet, "max_det %d outside (0, %d]", max_det, kMaxDet);
+  if (B == 0) return RV_OK;
+  ScaleArgs sc;
+  sc.gain = scale5[0];
+  sc.pad_x = scale5[1];
+  sc.pad_y = scale5[2];
+  sc.clip_w = scale5[3];
+  sc.clip_h = scale5[4];
+  const size_t smem = rv_nms_smem_bytes();
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)smem);
+    attr = true;
+  }
+  nms_kernel<<<B, 1024, smem, as_stream(stream)>>>((const Cand*)cand, cand_n, cap, max_wh,
+                                                    (double)iou, max_det, sc, keep_mask4, out,
+                                                    out_n);
+  return launch_status("rv_nms_postprocess");
+}
+
+extern "C" int rv_candidates_from_raw(const float* raw, int B, int nc, int A, float conf,
+                                      void* cand, int cap, int* cand_n, void* stream) {
+  RV_CHECK_ARG(raw && cand && cand_n, "null pointer");
+  RV_CHECK_ARG(B >= 0 && nc > 0 && A > 0 && A < 65536 && cap > 0, "bad raw shape");
+  if (B == 0) return RV_OK;
+  hipStream_t s = as_stream(stream);
+  hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * B, s);
+  if (e != hipSuccess) {
+    set_error("memset: %s", hipGetErrorString(e));
+    return -(int)e;
+  }
+  raw_candidates_kernel<<<dim3(ceil_div(A, 256), B), 256, 0, s>>>(raw, nc, A, conf, (Cand*)cand,
+                                                                  cap, cand_n);
+  return launch_status("rv_candidates_from_raw");
+}

@@ -1,0 +1,588 @@
+// YOLOv8 model plan + C ABI (the detector backend behind
+// src/detect/yolo_ultralytics.py:7-53, restating the Ultralytics yolov8.yaml
+// graph: Conv / C2f / SPPF / Detect(DFL)).
+//
+// The plan is built natively here: the canonical conv list (Ultralytics
+// state_dict order, BN already fused into conv weight + bias), the weight
+// packer, the activation-buffer layout in one caller-owned HBM workspace, and
+// the launch sequence of a forward.  Concats are free (producers write into
+// channel slices of the concat buffers); nearest-2x upsamples are extra
+// epilogue writes of the producing conv.
+#include <string>
+#include <vector>
+#include <cstring>
+#include <cmath>
+#include "conv.h"
+
+namespace rv {
+
+struct ConvSpec {
+  std::string name;
+  int cin, cout, k, s, act;
+  size_t w_off = 0, b_off = 0;  // byte offsets in the packed blob
+};
+
+struct Variant {
+  int c1, c2, c3, c4, c5;   // backbone widths (P1..P5)
+  int h12, h15, h18, h21;   // head widths
+  int nb, nm;               // C2f repeats for "3" and "6"
+  int c2d, c3d;             // Detect branch widths
+  int nc = 80, reg = 16;
+};
+
+static int make_div8(double x) { return (int)(std::ceil(x / 8.0) * 8); }
+
+static bool variant_widths(int variant, Variant& v) {
+  // yolov8.yaml scales: n [0.33, 0.25, 1024], s [0.33, 0.50, 1024],
+  // m [0.67, 0.75, 768], l [1.00, 1.00, 512], x [1.00, 1.25, 512]
+  static const double S[5][3] = {{0.33, 0.25, 1024}, {0.33, 0.50, 1024}, {0.67, 0.75, 768},
+                                 {1.00, 1.00, 512},  {1.00, 1.25, 512}};
+  if (variant < 0 || variant > 4) return false;
+  const double d = S[variant][0], w = S[variant][1], mc = S[variant][2];
+  auto ch = [&](int c) { return make_div8(std::min((double)c, mc) * w); };
+  auto rep = [&](int n) { return std::max((int)std::lround(n * d), 1); };
+  v.c1 = ch(64);
+  v.c2 = ch(128);
+  v.c3 = ch(256);
+  v.c4 = ch(512);
+  v.c5 = ch(1024);
+  v.h12 = ch(512);
+  v.h15 = ch(256);
+  v.h18 = ch(512);
+  v.h21 = ch(1024);
+  v.nb = rep(3);
+  v.nm = rep(6);
+  v.c2d = std::max(std::max(16, v.h15 / 4), v.reg * 4);
+  v.c3d = std::max(v.h15, std::min(v.nc, 100));
+  return true;
+}
+
+struct ModelDef {
+  Variant v;
+  std::vector<ConvSpec> convs;
+  int add(const std::string& n, int ci, int co, int k, int s, int act = 1) {
+    ConvSpec c;
+    c.name = n;
+    c.cin = ci;
+    c.cout = co;
+    c.k = k;
+    c.s = s;
+    c.act = act;
+    convs.push_back(c);
+    return (int)convs.size() - 1;
+  }
+  void c2f(const std::string& p, int c1, int c2, int n) {
+    const int c = c2 / 2;
+    add(p + ".cv1", c1, 2 * c, 1, 1);
+    add(p + ".cv2", (2 + n) * c, c2, 1, 1);
+    for (int i = 0; i < n; ++i) {
+      add(p + ".m." + std::to_string(i) + ".cv1", c, c, 3, 1);
+      add(p + ".m." + std::to_string(i) + ".cv2", c, c, 3, 1);
+    }
+  }
+  int find(const std::string& n) const {
+    for (size_t i = 0; i < convs.size(); ++i)
+      if (convs[i].name == n) return (int)i;
+    return -1;
+  }
+};
+
+static bool build_def(int variant, ModelDef& m) {
+  if (!variant_widths(variant, m.v)) return false;
+  const Variant& v = m.v;
+  m.add("model.0", 3, v.c1, 3, 2);
+  m.add("model.1", v.c1, v.c2, 3, 2);
+  m.c2f("model.2", v.c2, v.c2, v.nb);
+  m.add("model.3", v.c2, v.c3, 3, 2);
+  m.c2f("model.4", v.c3, v.c3, v.nm);
+  m.add("model.5", v.c3, v.c4, 3, 2);
+  m.c2f("model.6", v.c4, v.c4, v.nm);
+  m.add("model.7", v.c4, v.c5, 3, 2);
+  m.c2f("model.8", v.c5, v.c5, v.nb);
+  m.add("model.9.cv1", v.c5, v.c5 / 2, 1, 1);
+  m.add("model.9.cv2", v.c5 / 2 * 4, v.c5, 1, 1);
+  m.c2f("model.12", v.c5 + v.c4, v.h12, v.nb);
+  m.c2f("model.15", v.h12 + v.c3, v.h15, v.nb);
+  m.add("model.16", v.h15, v.h15, 3, 2);
+  m.c2f("model.18", v.h15 + v.h12, v.h18, v.nb);
+  m.add("model.19", v.h18, v.h18, 3, 2);
+  m.c2f("model.21", v.h18 + v.c5, v.h21, v.nb);
+  const int chs[3] = {v.h15, v.h18, v.h21};
+  for (int i = 0; i < 3; ++i) {
+    const std::string p = "model.22.cv2." + std::to_string(i);
+    m.add(p + ".0", chs[i], v.c2d, 3, 1);
+    m.add(p + ".1", v.c2d, v.c2d, 3, 1);
+    m.add(p + ".2", v.c2d, 4 * v.reg, 1, 1, 0);
+  }
+  for (int i = 0; i < 3; ++i) {
+    const std::string p = "model.22.cv3." + std::to_string(i);
+    m.add(p + ".0", chs[i], v.c3d, 3, 1);
+    m.add(p + ".1", v.c3d, v.c3d, 3, 1);
+    m.add(p + ".2", v.c3d, v.nc, 1, 1, 0);
+  }
+  // packed layout: conv 0 keeps f32 OIHW (VALU conv), the rest bf16
+  // [Cout_pad16][ky][kx][Cin_pad32]; biases f32 [Cout_pad16]; 256-B aligned
+  size_t off = 0;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  for (size_t i = 0; i < m.convs.size(); ++i) {
+    ConvSpec& c = m.convs[i];
+    const int cop = (c.cout + 15) & ~15;
+    const int cip = (c.cin + 31) & ~31;
+    c.w_off = off;
+    off = al(off + (i == 0 ? (size_t)c.cout * c.cin * c.k * c.k * 4
+                           : (size_t)cop * c.k * c.k * cip * 2));
+    c.b_off = off;
+    off = al(off + (size_t)cop * 4);
+  }
+  return true;
+}
+
+static size_t packed_bytes(const ModelDef& m) {
+  const ConvSpec& c = m.convs.back();
+  return ((c.b_off + (size_t)((c.cout + 15) & ~15) * 4) + 255) & ~(size_t)255;
+}
+
+static size_t flat_floats(const ModelDef& m) {
+  size_t n = 0;
+  for (const ConvSpec& c : m.convs) n += (size_t)c.cout * c.cin * c.k * c.k + c.cout;
+  return n;
+}
+
+static uint16_t host_f2bf(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7F800000u) == 0x7F800000u) return (uint16_t)(u >> 16);  // inf/nan
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// ---------------------------------------------------------------------------
+// Plan: activation buffers (element offsets into the bf16 workspace, per B)
+// ---------------------------------------------------------------------------
+struct View {
+  int buf;  // buffer id
+  int cs, co;
+};
+
+struct Buf {
+  size_t elems_per_img;
+  bool f32;
+  size_t off_bytes;  // filled per B
+};
+
+struct TraceRec {
+  int conv, in_buf, in_cs, in_co, Hin, Win, Ho, Wo;
+  int out0_buf, out0_cs, out0_co, up0, out1_buf, out1_cs, out1_co, up1;
+  int res_buf, res_cs, res_co, pad;
+};
+
+struct Model {
+  ModelDef def;
+  std::vector<TraceRec> trace;  // conv launches of the last forward
+  std::vector<std::pair<std::string, int>> tmps;  // bottleneck temp buffer per "prefix.m.i"
+  int tmp_of(const std::string& k) const {
+    for (auto& t : tmps)
+      if (t.first == k) return t.second;
+    return -1;
+  }
+  const uint8_t* dev = nullptr;  // packed weights (caller-owned device memory)
+  int max_B = 0, H = 0, W = 0;
+  std::vector<Buf> bufs;
+  int nA = 0;
+  int map_h[6], map_w[6];  // stride 2^i maps
+
+  std::vector<int> buf_h, buf_w, buf_c;
+  int newbuf(int s, int c, bool f32 = false) {
+    Buf b;
+    b.elems_per_img = (size_t)map_h[s] * map_w[s] * c;
+    b.f32 = f32;
+    b.off_bytes = 0;
+    bufs.push_back(b);
+    buf_h.push_back(map_h[s]);
+    buf_w.push_back(map_w[s]);
+    buf_c.push_back(c);
+    return (int)bufs.size() - 1;
+  }
+  // buffer ids
+  int X0, X1, C2, X2, X3, C4, CAT14, X5, C6, CAT11, X7, C8, X8, SP, CAT20, C12, CAT17, C15,
+      X15, C18, X18, C21, X21;
+  int DA[3], DB[3], HD[3];
+
+  size_t ws_bytes(int B) const {
+    size_t off = 0;
+    for (const Buf& b : bufs)
+      off = (off + b.elems_per_img * B * (b.f32 ? 4 : 2) + 255) & ~(size_t)255;
+    return off;
+  }
+};
+
+static void plan(Model& M) {
+  const Variant& v = M.def.v;
+  for (int i = 0; i < 6; ++i) {
+    M.map_h[i] = M.H >> i;
+    M.map_w[i] = M.W >> i;
+  }
+  M.X0 = M.newbuf(1, v.c1);
+  M.X1 = M.newbuf(2, v.c2);
+  M.C2 = M.newbuf(2, (2 + v.nb) * (v.c2 / 2));
+  M.X2 = M.newbuf(2, v.c2);
+  M.X3 = M.newbuf(3, v.c3);
+  M.C4 = M.newbuf(3, (2 + v.nm) * (v.c3 / 2));
+  M.CAT14 = M.newbuf(3, v.h12 + v.c3);
+  M.X5 = M.newbuf(4, v.c4);
+  M.C6 = M.newbuf(4, (2 + v.nm) * (v.c4 / 2));
+  M.CAT11 = M.newbuf(4, v.c5 + v.c4);
+  M.X7 = M.newbuf(5, v.c5);
+  M.C8 = M.newbuf(5, (2 + v.nb) * (v.c5 / 2));
+  M.X8 = M.newbuf(5, v.c5);
+  M.SP = M.newbuf(5, 4 * (v.c5 / 2));
+  M.CAT20 = M.newbuf(5, v.h18 + v.c5);
+  M.C12 = M.newbuf(4, (2 + v.nb) * (v.h12 / 2));
+  M.CAT17 = M.newbuf(4, v.h15 + v.h12);
+  M.C15 = M.newbuf(3, (2 + v.nb) * (v.h15 / 2));
+  M.X15 = M.newbuf(3, v.h15);
+  M.C18 = M.newbuf(4, (2 + v.nb) * (v.h18 / 2));
+  M.X18 = M.newbuf(4, v.h18);
+  M.C21 = M.newbuf(5, (2 + v.nb) * (v.h21 / 2));
+  M.X21 = M.newbuf(5, v.h21);
+  for (int i = 0; i < 3; ++i) {
+    M.DA[i] = M.newbuf(3 + i, v.c2d + v.c3d);
+    M.DB[i] = M.newbuf(3 + i, v.c2d + v.c3d);
+    M.HD[i] = M.newbuf(3 + i, 4 * v.reg + v.nc, true);
+  }
+  // one temp per bottleneck (its first conv's output): no buffer is ever
+  // overwritten inside a forward, so every layer stays inspectable
+  struct C2fDef {
+    const char* p;
+    int level, c2, n;
+  };
+  const C2fDef cs[] = {{"model.2", 2, v.c2, v.nb},  {"model.4", 3, v.c3, v.nm},
+                       {"model.6", 4, v.c4, v.nm},  {"model.8", 5, v.c5, v.nb},
+                       {"model.12", 4, v.h12, v.nb}, {"model.15", 3, v.h15, v.nb},
+                       {"model.18", 4, v.h18, v.nb}, {"model.21", 5, v.h21, v.nb}};
+  for (const C2fDef& c : cs)
+    for (int i = 0; i < c.n; ++i)
+      M.tmps.push_back({std::string(c.p) + ".m." + std::to_string(i), M.newbuf(c.level, c.c2 / 2)});
+  M.nA = M.map_h[3] * M.map_w[3] + M.map_h[4] * M.map_w[4] + M.map_h[5] * M.map_w[5];
+}
+
+struct Exec {
+  Model* M;
+  uint8_t* ws;
+  int B;
+  hipStream_t s;
+  std::vector<size_t> off;
+  int status = 0;
+
+  void* ptr(int buf) const { return ws + off[buf]; }
+  const bf16_t* wptr(const ConvSpec& c) const { return (const bf16_t*)(M->dev + c.w_off); }
+  const float* bptr(const ConvSpec& c) const { return (const float*)(M->dev + c.b_off); }
+
+  // conv `name`: input view at map level li -> up to two output views
+  void conv(const std::string& name, View in, int li, View o0, int up0 = 0, View o1 = {-1, 0, 0},
+            int up1 = 0, View res = {-1, 0, 0}) {
+    if (status) return;
+    const int idx = M->def.find(name);
+    if (idx < 0) {
+      set_error("plan: unknown conv %s", name.c_str());
+      status = RV_EINVAL;
+      return;
+    }
+    const ConvSpec& c = M->def.convs[idx];
+    ConvArgs a;
+    memset(&a, 0, sizeof(a));
+    a.in = (const bf16_t*)ptr(in.buf);
+    a.in_cs = in.cs;
+    a.in_co = in.co;
+    a.Hin = M->map_h[li];
+    a.Win = M->map_w[li];
+    a.Cin = c.cin;
+    a.w = wptr(c);
+    a.bias = bptr(c);
+    a.Cout = c.cout;
+    a.k = c.k;
+    a.stride = c.s;
+    a.pad = c.k / 2;
+    a.Ho = (a.Hin + 2 * a.pad - c.k) / c.s + 1;
+    a.Wo = (a.Win + 2 * a.pad - c.k) / c.s + 1;
+    a.B = B;
+    a.out0 = ptr(o0.buf);
+    a.out0_cs = o0.cs;
+    a.out0_co = o0.co;
+    a.out0_up = up0;
+    if (o1.buf >= 0) {
+      a.out1 = ptr(o1.buf);
+      a.out1_cs = o1.cs;
+      a.out1_co = o1.co;
+      a.out1_up = up1;
+    }
+    a.out_f32 = M->bufs[o0.buf].f32 ? 1 : 0;
+    if (res.buf >= 0) {
+      a.res = (const bf16_t*)ptr(res.buf);
+      a.res_cs = res.cs;
+      a.res_co = res.co;
+    }
+    a.act = c.act;
+    TraceRec r;
+    memset(&r, 0, sizeof(r));
+    r.conv = idx;
+    r.in_buf = in.buf;
+    r.in_cs = in.cs;
+    r.in_co = in.co;
+    r.Hin = a.Hin;
+    r.Win = a.Win;
+    r.Ho = a.Ho;
+    r.Wo = a.Wo;
+    r.out0_buf = o0.buf;
+    r.out0_cs = o0.cs;
+    r.out0_co = o0.co;
+    r.up0 = up0;
+    r.out1_buf = o1.buf;
+    r.out1_cs = o1.cs;
+    r.out1_co = o1.co;
+    r.up1 = up1;
+    r.res_buf = res.buf;
+    r.res_cs = res.cs;
+    r.res_co = res.co;
+    M->trace.push_back(r);
+    status = launch_conv(a, s);
+  }
+
+  // C2f(prefix): in view (map li) -> concat buffer cb -> outputs
+  void c2f(const std::string& p, View in, int li, int cb, int c2, int n, bool shortcut, View o0,
+           int up0 = 0, View o1 = {-1, 0, 0}, int up1 = 0) {
+    const int c = c2 / 2;
+    const int cs = (2 + n) * c;
+    conv(p + ".cv1", in, li, View{cb, cs, 0});
+    for (int i = 0; i < n; ++i) {
+      const View bin{cb, cs, (1 + i) * c};
+      const std::string q = p + ".m." + std::to_string(i);
+      const int tmp = M->tmp_of(q);
+      conv(q + ".cv1", bin, li, View{tmp, c, 0});
+      conv(q + ".cv2", View{tmp, c, 0}, li, View{cb, cs, (2 + i) * c}, 0, {-1, 0, 0}, 0,
+           shortcut ? bin : View{-1, 0, 0});
+    }
+    conv(p + ".cv2", View{cb, cs, 0}, li, o0, up0, o1, up1);
+  }
+};
+
+}  // namespace rv
+
+using namespace rv;
+
+extern "C" int rv_yolo_num_convs(int variant) {
+  ModelDef m;
+  if (!build_def(variant, m)) return RV_EINVAL;
+  return (int)m.convs.size();
+}
+
+extern "C" int rv_yolo_conv_info(int variant, int idx, int* info, char* name, int name_cap) {
+  ModelDef m;
+  RV_CHECK_ARG(build_def(variant, m), "unknown variant %d", variant);
+  RV_CHECK_ARG(idx >= 0 && idx < (int)m.convs.size() && info, "bad conv index %d", idx);
+  const ConvSpec& c = m.convs[idx];
+  info[0] = c.cin;
+  info[1] = c.cout;
+  info[2] = c.k;
+  info[3] = c.s;
+  info[4] = c.act;
+  if (name && name_cap > 0) {
+    strncpy(name, c.name.c_str(), name_cap - 1);
+    name[name_cap - 1] = 0;
+  }
+  return RV_OK;
+}
+
+extern "C" size_t rv_yolo_flat_floats(int variant) {
+  ModelDef m;
+  if (!build_def(variant, m)) return 0;
+  return flat_floats(m);
+}
+
+extern "C" size_t rv_yolo_packed_bytes(int variant) {
+  ModelDef m;
+  if (!build_def(variant, m)) return 0;
+  return packed_bytes(m);
+}
+
+extern "C" int rv_yolo_pack(int variant, const float* flat, size_t n, void* host_out,
+                            size_t out_bytes) {
+  ModelDef m;
+  RV_CHECK_ARG(build_def(variant, m), "unknown variant %d", variant);
+  RV_CHECK_ARG(flat && host_out, "null pointer");
+  RV_CHECK_ARG(n == flat_floats(m), "flat weights: got %zu floats, need %zu", n, flat_floats(m));
+  RV_CHECK_ARG(out_bytes >= packed_bytes(m), "packed buffer too small");
+  uint8_t* out = (uint8_t*)host_out;
+  memset(out, 0, packed_bytes(m));
+  const float* p = flat;
+  for (size_t i = 0; i < m.convs.size(); ++i) {
+    const ConvSpec& c = m.convs[i];
+    const size_t nw = (size_t)c.cout * c.cin * c.k * c.k;
+    const float* w = p;
+    const float* b = p + nw;
+    p += nw + c.cout;
+    if (i == 0) {
+      memcpy(out + c.w_off, w, nw * 4);
+    } else {
+      const int cip = (c.cin + 31) & ~31;
+      uint16_t* dst = (uint16_t*)(out + c.w_off);
+      for (int o = 0; o < c.cout; ++o)
+        for (int ky = 0; ky < c.k; ++ky)
+          for (int kx = 0; kx < c.k; ++kx)
+            for (int ci = 0; ci < c.cin; ++ci)
+              dst[((size_t)o * c.k * c.k + ky * c.k + kx) * cip + ci] =
+                  host_f2bf(w[(((size_t)o * c.cin + ci) * c.k + ky) * c.k + kx]);
+    }
+    memcpy(out + c.b_off, b, (size_t)c.cout * 4);
+  }
+  return RV_OK;
+}
+
+extern "C" int rv_yolo_create(int variant, const void* dev_packed, int max_B, int in_h, int in_w,
+                              void** handle) {
+  RV_CHECK_ARG(handle && dev_packed, "null pointer");
+  RV_CHECK_ARG(max_B > 0 && in_h > 0 && in_w > 0 && in_h % 32 == 0 && in_w % 32 == 0,
+               "input %dx%d must be positive multiples of 32", in_h, in_w);
+  Model* M = new Model();
+  if (!build_def(variant, M->def)) {
+    delete M;
+    set_error("unknown variant %d", variant);
+    return RV_EINVAL;
+  }
+  M->dev = (const uint8_t*)dev_packed;
+  M->max_B = max_B;
+  M->H = in_h;
+  M->W = in_w;
+  plan(*M);
+  *handle = M;
+  return RV_OK;
+}
+
+extern "C" int rv_yolo_destroy(void* h) {
+  delete (Model*)h;
+  return RV_OK;
+}
+
+extern "C" size_t rv_yolo_ws_bytes(void* h, int B) {
+  if (!h || B <= 0) return 0;
+  return ((Model*)h)->ws_bytes(B);
+}
+
+extern "C" int rv_yolo_num_anchors(void* h) { return h ? ((Model*)h)->nA : 0; }
+
+extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
+                               float* raw_out, float conf, void* cand, int cand_cap, int* cand_n,
+                               void* stream) {
+  RV_CHECK_ARG(h && lb && ws, "null pointer");
+  Model* M = (Model*)h;
+  RV_CHECK_ARG(B > 0 && B <= M->max_B, "B=%d outside (0, %d]", B, M->max_B);
+  RV_CHECK_ARG(ws_bytes >= M->ws_bytes(B), "workspace %zu < %zu bytes", ws_bytes, M->ws_bytes(B));
+  RV_CHECK_ARG(!cand || (cand_n && cand_cap > 0), "candidate buffers incomplete");
+  const Variant& v = M->def.v;
+  Exec E;
+  E.M = M;
+  E.ws = (uint8_t*)ws;
+  E.B = B;
+  E.s = as_stream(stream);
+  size_t off = 0;
+  for (const Buf& b : M->bufs) {
+    E.off.push_back(off);
+    off = (off + b.elems_per_img * B * (b.f32 ? 4 : 2) + 255) & ~(size_t)255;
+  }
+  M->trace.clear();
+  if (cand_n) {
+    hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * B, E.s);
+    if (e != hipSuccess) {
+      set_error("memset: %s", hipGetErrorString(e));
+      return -(int)e;
+    }
+  }
+  // backbone
+  const ConvSpec& c0 = M->def.convs[0];
+  int st = launch_conv0(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
+                        (const float*)(M->dev + c0.b_off), c0.cout, (bf16_t*)E.ptr(M->X0), v.c1,
+                        E.s);
+  if (st) return st;
+  E.conv("model.1", View{M->X0, v.c1, 0}, 1, View{M->X1, v.c2, 0});
+  E.c2f("model.2", View{M->X1, v.c2, 0}, 2, M->C2, v.c2, v.nb, true, View{M->X2, v.c2, 0});
+  E.conv("model.3", View{M->X2, v.c2, 0}, 2, View{M->X3, v.c3, 0});
+  const int cat14 = v.h12 + v.c3, cat11 = v.c5 + v.c4, cat20 = v.h18 + v.c5,
+            cat17 = v.h15 + v.h12;
+  E.c2f("model.4", View{M->X3, v.c3, 0}, 3, M->C4, v.c3, v.nm, true,
+        View{M->CAT14, cat14, v.h12});
+  E.conv("model.5", View{M->CAT14, cat14, v.h12}, 3, View{M->X5, v.c4, 0});
+  E.c2f("model.6", View{M->X5, v.c4, 0}, 4, M->C6, v.c4, v.nm, true,
+        View{M->CAT11, cat11, v.c5});
+  E.conv("model.7", View{M->CAT11, cat11, v.c5}, 4, View{M->X7, v.c5, 0});
+  E.c2f("model.8", View{M->X7, v.c5, 0}, 5, M->C8, v.c5, v.nb, true, View{M->X8, v.c5, 0});
+  // SPPF
+  const int sc = v.c5 / 2;
+  E.conv("model.9.cv1", View{M->X8, v.c5, 0}, 5, View{M->SP, 4 * sc, 0});
+  if (E.status) return E.status;
+  st = launch_sppf_pool((bf16_t*)E.ptr(M->SP), B, M->map_h[5], M->map_w[5], sc, E.s);
+  if (st) return st;
+  E.conv("model.9.cv2", View{M->SP, 4 * sc, 0}, 5, View{M->CAT20, cat20, v.h18}, 0,
+         View{M->CAT11, cat11, 0}, 1);
+  // head
+  E.c2f("model.12", View{M->CAT11, cat11, 0}, 4, M->C12, v.h12, v.nb, false,
+        View{M->CAT17, cat17, v.h15}, 0, View{M->CAT14, cat14, 0}, 1);
+  E.c2f("model.15", View{M->CAT14, cat14, 0}, 3, M->C15, v.h15, v.nb, false,
+        View{M->X15, v.h15, 0});
+  E.conv("model.16", View{M->X15, v.h15, 0}, 3, View{M->CAT17, cat17, 0});
+  E.c2f("model.18", View{M->CAT17, cat17, 0}, 4, M->C18, v.h18, v.nb, false,
+        View{M->X18, v.h18, 0});
+  E.conv("model.19", View{M->X18, v.h18, 0}, 4, View{M->CAT20, cat20, 0});
+  E.c2f("model.21", View{M->CAT20, cat20, 0}, 5, M->C21, v.h21, v.nb, false,
+        View{M->X21, v.h21, 0});
+  // Detect
+  const View P[3] = {View{M->X15, v.h15, 0}, View{M->X18, v.h18, 0}, View{M->X21, v.h21, 0}};
+  const int dcs = v.c2d + v.c3d, hcs = 4 * v.reg + v.nc;
+  for (int i = 0; i < 3; ++i) {
+    const std::string a = "model.22.cv2." + std::to_string(i), c = "model.22.cv3." + std::to_string(i);
+    E.conv(a + ".0", P[i], 3 + i, View{M->DA[i], dcs, 0});
+    E.conv(c + ".0", P[i], 3 + i, View{M->DA[i], dcs, v.c2d});
+    E.conv(a + ".1", View{M->DA[i], dcs, 0}, 3 + i, View{M->DB[i], dcs, 0});
+    E.conv(c + ".1", View{M->DA[i], dcs, v.c2d}, 3 + i, View{M->DB[i], dcs, v.c2d});
+    E.conv(a + ".2", View{M->DB[i], dcs, 0}, 3 + i, View{M->HD[i], hcs, 0});
+    E.conv(c + ".2", View{M->DB[i], dcs, v.c2d}, 3 + i, View{M->HD[i], hcs, 4 * v.reg});
+  }
+  if (E.status) return E.status;
+  HeadLevel hl[3];
+  for (int i = 0; i < 3; ++i) {
+    hl[i].logits = (const float*)E.ptr(M->HD[i]);
+    hl[i].H = M->map_h[3 + i];
+    hl[i].W = M->map_w[3 + i];
+    hl[i].cs = hcs;
+    hl[i].stride = (float)(8 << i);
+  }
+  return launch_detect_decode(hl, 3, B, v.nc, v.reg, conf, raw_out, (Cand*)cand, cand_cap, cand_n,
+                              E.s);
+}
+
+// ---- introspection (parity tests / debugging) ------------------------------
+extern "C" int rv_yolo_num_buffers(void* h) { return h ? (int)((Model*)h)->bufs.size() : 0; }
+
+extern "C" int rv_yolo_buffer_info(void* h, int B, int buf, int* info, size_t* off_bytes) {
+  RV_CHECK_ARG(h && info && off_bytes && B > 0, "bad args");
+  Model* M = (Model*)h;
+  RV_CHECK_ARG(buf >= 0 && buf < (int)M->bufs.size(), "bad buffer %d", buf);
+  size_t off = 0;
+  for (int i = 0; i < buf; ++i)
+    off = (off + M->bufs[i].elems_per_img * B * (M->bufs[i].f32 ? 4 : 2) + 255) & ~(size_t)255;
+  *off_bytes = off;
+  info[0] = M->buf_h[buf];
+  info[1] = M->buf_w[buf];
+  info[2] = M->buf_c[buf];
+  info[3] = M->bufs[buf].f32 ? 1 : 0;
+  return RV_OK;
+}
+
+// 20 ints per conv launch of the last forward; returns the record count
+extern "C" int rv_yolo_trace(void* h, int* recs, int max_recs) {
+  if (!h) return RV_EINVAL;
+  Model* M = (Model*)h;
+  const int n = (int)M->trace.size();
+  if (recs)
+    for (int i = 0; i < n && i < max_recs; ++i) memcpy(recs + 20 * i, &M->trace[i], 20 * sizeof(int));
+  return n;
+}

@@ -38,6 +38,34 @@ _SIGS = {
     "rv_letterbox_geometry": (c_int, [c_int, c_int, c_int, c_int, POINTER(c_int)]),
     "rv_letterbox_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                 POINTER(c_int), c_void_p]),
+    # detect
+    "rv_yolo_num_convs": (c_int, [c_int]),
+    "rv_yolo_conv_info": (c_int, [c_int, c_int, POINTER(c_int), ctypes.c_char_p, c_int]),
+    "rv_yolo_flat_floats": (c_size_t, [c_int]),
+    "rv_yolo_packed_bytes": (c_size_t, [c_int]),
+    "rv_yolo_pack": (c_int, [c_int, c_void_p, c_size_t, c_void_p, c_size_t]),
+    "rv_yolo_create": (c_int, [c_int, c_void_p, c_int, c_int, c_int, POINTER(c_void_p)]),
+    "rv_yolo_destroy": (c_int, [c_void_p]),
+    "rv_yolo_ws_bytes": (c_size_t, [c_void_p, c_int]),
+    "rv_yolo_num_anchors": (c_int, [c_void_p]),
+    "rv_yolo_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_float,
+                                c_void_p, c_int, c_void_p, c_void_p]),
+    "rv_yolo_num_buffers": (c_int, [c_void_p]),
+    "rv_yolo_buffer_info": (c_int, [c_void_p, c_int, c_int, POINTER(c_int), POINTER(c_size_t)]),
+    "rv_yolo_trace": (c_int, [c_void_p, c_void_p, c_int]),
+    "rv_nms_smem_bytes": (c_size_t, []),
+    "rv_nms_postprocess": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_int, c_float,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rv_candidates_from_raw": (c_int, [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int,
+                                       c_void_p, c_void_p]),
+    # track
+    "rv_sort_state_bytes": (c_size_t, [c_int, c_int]),
+    "rv_sort_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "rv_sort_init": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "rv_sort_update": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                               c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rv_sort_export": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 
@@ -74,7 +102,8 @@ def check(status: int, what: str = "") -> None:
         raise RVError(f"{what or 'rvhip'} failed with status {status}: {msg}")
 
 
-_NOCHECK = {"rv_abi_version", "rv_clahe_median_fits"}
+_NOCHECK = {"rv_abi_version", "rv_clahe_median_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
+            "rv_yolo_num_buffers", "rv_yolo_trace"}
 
 
 def call(name: str, *args) -> int:

@@ -1,0 +1,200 @@
+"""HIP YOLOv8 detector backend (drop-in for src/detect/yolo_ultralytics.py).
+
+``YoloEngine`` is the batched device path: letterbox (rv_letterbox_u8) ->
+YOLOv8 forward on MFMA with fused decode/candidate filter (rv_yolo_forward) ->
+batched NMS + scale_boxes + class filter (rv_nms_postprocess).  Everything
+stays on the GPU; only ``to_detections`` copies the (B, max_det, 6) result to
+the host to build ``Detection`` objects, matching yolo_ultralytics.py:44-52.
+
+``YOLOHip`` wraps it behind the reference's ``Detector`` interface with the
+same config keys (model, device, conf_thres, iou_thres, max_det,
+classes_keep; yolo_ultralytics.py:15-24).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import _lib, kernels
+from .._lib import call, ptr, stream_ptr
+from .base import Detector
+from .types import Detection
+from .weights import COCO80, load_weights, pack, synthetic_weights, variant_of
+
+CAND_BYTES = 32
+
+
+def scale_boxes_params(img1_hw, img0_hw):
+    """Ultralytics ops.scale_boxes(img1_shape, boxes, img0_shape) constants:
+    (gain, pad_x, pad_y) with python-float gain and python round()."""
+    gain = min(img1_hw[0] / img0_hw[0], img1_hw[1] / img0_hw[1])
+    pad_x = round((img1_hw[1] - img0_hw[1] * gain) / 2 - 0.1)
+    pad_y = round((img1_hw[0] - img0_hw[0] * gain) / 2 - 0.1)
+    return gain, pad_x, pad_y
+
+
+def class_mask(classes_keep: Sequence[int]) -> Optional[np.ndarray]:
+    keep = set(int(x) for x in classes_keep)
+    if not keep:
+        return None
+    m = np.zeros(4, np.uint32)
+    for c in keep:
+        if 0 <= c < 128:
+            m[c >> 5] |= np.uint32(1 << (c & 31))
+    return m
+
+
+class YoloEngine:
+    """Batched letterbox -> YOLOv8 -> NMS for frames of one (H, W)."""
+
+    def __init__(self, variant: int, flat_weights: np.ndarray, max_batch: int, frame_hw,
+                 imgsz: int = 640, stride: int = 32, conf: float = 0.25, iou: float = 0.7,
+                 max_det: int = 100, classes_keep: Sequence[int] = (), max_wh: float = 7680.0,
+                 device="cuda"):
+        self.device = torch.device(device)
+        self.variant = variant
+        self.H, self.W = int(frame_hw[0]), int(frame_hw[1])
+        self.max_batch = int(max_batch)
+        self.conf, self.iou, self.max_det, self.max_wh = float(conf), float(iou), int(max_det), \
+            float(max_wh)
+        self.geo = kernels.letterbox_geometry(self.H, self.W, imgsz, stride)
+        self.in_h, self.in_w = self.geo[0], self.geo[1]
+        self.packed = torch.from_numpy(pack(variant, flat_weights)).to(self.device)
+        h = ctypes.c_void_p()
+        call("rv_yolo_create", variant, ptr(self.packed), self.max_batch, self.in_h, self.in_w,
+             ctypes.byref(h))
+        self._h = h
+        lib = _lib.load()
+        self.A = lib.rv_yolo_num_anchors(h)
+        self.nc = 80
+        self.ws_bytes = lib.rv_yolo_ws_bytes(h, self.max_batch)
+        dev = self.device
+        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
+        self.lb = torch.empty((self.max_batch, self.in_h, self.in_w, 3), dtype=torch.uint8,
+                              device=dev)
+        self.cap = self.A
+        self.cand = torch.empty((self.max_batch, self.cap, CAND_BYTES // 4), dtype=torch.float32,
+                                device=dev)
+        self.cand_n = torch.zeros(self.max_batch, dtype=torch.int32, device=dev)
+        self.dets = torch.zeros((self.max_batch, self.max_det, 6), dtype=torch.float32, device=dev)
+        self.det_n = torch.zeros(self.max_batch, dtype=torch.int32, device=dev)
+        gain, px, py = scale_boxes_params((self.in_h, self.in_w), (self.H, self.W))
+        self.scale5 = torch.tensor([gain, px, py, self.W, self.H], dtype=torch.float32, device=dev)
+        m = class_mask(classes_keep)
+        self.keep = None if m is None else torch.from_numpy(m.view(np.int32)).to(dev)
+
+    def close(self):
+        if self._h:
+            _lib.load().rv_yolo_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def letterbox(self, frames: torch.Tensor) -> torch.Tensor:
+        B = frames.shape[0]
+        return kernels.letterbox(frames, self.geo, out=self.lb[:B])
+
+    def forward_raw(self, lb: torch.Tensor, raw: Optional[torch.Tensor] = None,
+                    candidates: bool = True):
+        B = lb.shape[0]
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} > max_batch {self.max_batch}")
+        lb = lb.contiguous()
+        call("rv_yolo_forward", self._h, ptr(lb), B, ptr(self.ws), self.ws_bytes, ptr(raw),
+             self.conf, ptr(self.cand) if candidates else None, self.cap,
+             ptr(self.cand_n) if candidates else None, stream_ptr())
+        return raw
+
+    def nms(self, B: int):
+        call("rv_nms_postprocess", ptr(self.cand), ptr(self.cand_n), B, self.cap, self.iou,
+             self.max_det, self.max_wh, ptr(self.scale5), ptr(self.keep), ptr(self.dets),
+             ptr(self.det_n), stream_ptr())
+        return self.dets[:B], self.det_n[:B]
+
+    def nms_from_raw(self, raw: torch.Tensor):
+        """Reference-layout entry (B, 4+nc, A) -> NMS (parity tests)."""
+        B, C, A = raw.shape
+        raw = raw.contiguous()
+        call("rv_candidates_from_raw", ptr(raw), B, C - 4, A, self.conf, ptr(self.cand), self.cap,
+             ptr(self.cand_n), stream_ptr())
+        return self.nms(B)
+
+    def run(self, frames: torch.Tensor):
+        """(B,H,W,3) u8 device frames -> (dets (B,max_det,6), counts (B,)) on device."""
+        if frames.dim() == 3:
+            frames = frames.unsqueeze(0)
+        B = frames.shape[0]
+        self.forward_raw(self.letterbox(frames))
+        return self.nms(B)
+
+    @staticmethod
+    def to_detections(dets: torch.Tensor, det_n: torch.Tensor, names=COCO80) -> List[List[Detection]]:
+        d = dets.cpu().numpy()
+        n = det_n.cpu().numpy()
+        out = []
+        for b in range(d.shape[0]):
+            lst = []
+            for r in d[b, :int(n[b])]:
+                k = int(r[5])
+                name = str(names[k]) if names is not None and 0 <= k < len(names) else str(k)
+                lst.append(Detection(float(r[0]), float(r[1]), float(r[2]), float(r[3]),
+                                     float(r[4]), k, name))
+            out.append(lst)
+        return out
+
+
+class YOLOHip(Detector):
+    """Config-compatible replacement of YOLOUltralytics (backend 'hip')."""
+
+    def __init__(self, cfg: Dict):
+        device = cfg.get("device", "auto")
+        self.device = torch.device("cuda:0" if device in ("auto", None, "cpu") else device)
+        if not torch.cuda.is_available():
+            raise RuntimeError("YOLOHip needs an MI355X (HIP device); there is no CPU fallback")
+        self.variant = variant_of(cfg.get("model", "yolov8n.pt"))
+        wpath = cfg.get("weights")
+        self.flat = (load_weights(wpath, self.variant) if wpath else
+                     synthetic_weights(self.variant, seed=int(cfg.get("seed", 0))))
+        self.conf = float(cfg.get("conf_thres", 0.25))
+        self.iou = float(cfg.get("iou_thres", 0.7))
+        self.max_det = int(cfg.get("max_det", 100))
+        self.keep = [int(x) for x in cfg.get("classes_keep", [])]
+        self.imgsz = int(cfg.get("imgsz", 640))
+        self.names = COCO80
+        self._engines: Dict = {}
+
+    def engine(self, H: int, W: int, max_batch: int = 1) -> YoloEngine:
+        key = (H, W)
+        e = self._engines.get(key)
+        if e is None or e.max_batch < max_batch:
+            e = YoloEngine(self.variant, self.flat, max_batch, (H, W), imgsz=self.imgsz,
+                           conf=self.conf, iou=self.iou, max_det=self.max_det,
+                           classes_keep=self.keep, device=self.device)
+            self._engines[key] = e
+        return e
+
+    def infer_batch(self, frames: torch.Tensor) -> List[List[Detection]]:
+        if frames.dim() == 3:
+            frames = frames.unsqueeze(0)
+        eng = self.engine(frames.shape[1], frames.shape[2], frames.shape[0])
+        dets, n = eng.run(frames)
+        return YoloEngine.to_detections(dets, n, self.names)
+
+    def infer(self, bgr) -> List[Detection]:
+        if isinstance(bgr, np.ndarray):
+            x = torch.from_numpy(np.ascontiguousarray(bgr)).to(self.device)
+        else:
+            x = bgr
+        return self.infer_batch(x)[0]
+
+    def close(self):
+        for e in self._engines.values():
+            e.close()
+        self._engines.clear()

@@ -1,0 +1,177 @@
+"""Layer-wise parity of the YOLOv8 HIP forward.
+
+Every conv launch of a forward is re-computed on the CPU from the GPU's own
+input activations (read back from the workspace; no buffer is reused inside
+a forward), with the same bf16 weights, in float64, then rounded like the
+kernel's epilogue.  This isolates each kernel from the error amplification of
+the full network (see test_detect_gpu.py).
+
+Tolerance per output element: |gpu - ref| <= 1 bf16 ulp of |ref| (+1e-3 of
+the layer RMS for cancellation near zero); fewer than 1e-4 of the elements
+may exceed that, and none by more than 2 ulp + 1e-2 RMS.  f32 head logits:
+|d| <= 1e-4 * RMS + 1e-5 |ref|.  SPPF pooling and the concat / upsample
+copies: exact.  Decode (DFL + dist2bbox + sigmoid) from the GPU's own head
+logits: |d| <= 1e-4 px / 1e-6.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import road_frame
+from oracle import cpu, yolo_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def bf16_to_f32(u16):
+    return (u16.astype(np.uint32) << 16).view(np.float32)
+
+
+def round_bf16(x):
+    return torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(torch.bfloat16).float().numpy()
+
+
+def ulp_bf16(x):
+    a = np.abs(x).astype(np.float32)
+    e = np.floor(np.log2(np.maximum(a, 2.0 ** -126)))
+    return 2.0 ** (e - 7)
+
+
+class Introspect:
+    def __init__(self, eng, B):
+        from rvs_amd import _lib
+        self.lib = _lib.load()
+        self.eng = eng
+        self.B = B
+        torch.cuda.synchronize()
+        self.ws = eng.ws.cpu().numpy()
+        n = self.lib.rv_yolo_trace(eng._h, None, 0)
+        recs = np.zeros(n * 20, np.int32)
+        self.lib.rv_yolo_trace(eng._h, recs.ctypes.data, n)
+        self.recs = recs.reshape(n, 20)
+        self.bufs = []
+        for i in range(self.lib.rv_yolo_num_buffers(eng._h)):
+            info = (ctypes.c_int * 4)()
+            off = ctypes.c_size_t()
+            self.lib.rv_yolo_buffer_info(eng._h, B, i, info, ctypes.byref(off))
+            self.bufs.append((info[0], info[1], info[2], info[3], off.value))
+
+    def view(self, buf):
+        h, w, c, f32, off = self.bufs[buf]
+        n = self.B * h * w * c
+        if f32:
+            return self.ws[off:off + 4 * n].view(np.float32).reshape(self.B, h, w, c)
+        return bf16_to_f32(self.ws[off:off + 2 * n].view(np.uint16)).reshape(self.B, h, w, c)
+
+
+def _setup(cuda, H, W, B, variant=0):
+    from rvs_amd.detect import weights
+    from rvs_amd.detect.yolo_hip import YoloEngine
+    flat = weights.synthetic_weights(variant, seed=1)
+    eng = YoloEngine(variant, flat, B, (H, W), device=cuda)
+    fr = np.stack([cpu.median(cpu.clahe_ycrcb(road_frame(H, W, seed=30 + b)), 3)
+                   for b in range(B)])
+    lb = eng.letterbox(torch.from_numpy(fr).to(cuda))
+    raw = torch.empty((B, 84, eng.A), dtype=torch.float32, device=cuda)
+    eng.forward_raw(lb, raw)
+    specs, _ = yolo_ref.conv_specs(variant)
+    params, off = {}, 0
+    for n, ci, co, k, s, act in specs:
+        nw = co * ci * k * k
+        params[n] = (flat[off:off + nw].reshape(co, ci, k, k), flat[off + nw:off + nw + co])
+        off += nw + co
+    return eng, Introspect(eng, B), specs, params, lb.cpu().numpy(), raw.cpu().numpy()
+
+
+@pytest.mark.parametrize("H,W,B", [(640, 640, 1), (1080, 1920, 2)])
+def test_every_conv_layerwise(cuda, H, W, B):
+    eng, ins, specs, params, lb, raw = _setup(cuda, H, W, B)
+    assert len(ins.recs) == len(specs) - 1  # all but model.0 go through conv_mfma
+    worst = []
+    for r in ins.recs:
+        (ci_, inb, incs, inco, Hin, Win, Ho, Wo, o0, o0cs, o0co, up0, o1, o1cs, o1co, up1,
+         rb, rcs, rco, _) = r.tolist()
+        name, cin, cout, k, s, act = specs[ci_]
+        w, b = params[name]
+        x = ins.view(inb)[..., inco:inco + cin]
+        xt = torch.from_numpy(np.ascontiguousarray(x.transpose(0, 3, 1, 2))).double()
+        wt = torch.from_numpy(round_bf16(w)).double()
+        y = F.conv2d(xt, wt, torch.from_numpy(b).double(), stride=s, padding=k // 2)
+        if act:
+            y = F.silu(y)
+        y = y.numpy().transpose(0, 2, 3, 1)
+        if rb >= 0:
+            y = y + ins.view(rb)[..., rco:rco + cout]
+        got = ins.view(o0)[..., o0co:o0co + cout]
+        if up0:
+            got = got[:, ::2, ::2]
+        rms = float(np.sqrt(np.mean(y ** 2))) + 1e-12
+        d = np.abs(got.astype(np.float64) - y)
+        if ins.bufs[o0][3]:  # f32 head logits
+            assert (d <= 1e-4 * rms + 1e-5 * np.abs(y)).all(), f"{name}: f32 max {d.max()}"
+            continue
+        tol1 = ulp_bf16(y) * 1.01 + 1e-3 * rms
+        frac = float((d > tol1).mean())
+        worst.append((frac, name))
+        assert frac < 1e-4, f"{name}: {frac:.2e} of elements beyond 1 ulp"
+        assert (d <= 2 * ulp_bf16(y) + 1e-2 * rms).all(), f"{name}: max dev {d.max()}"
+        if o1 >= 0:  # second destination (concat slice or upsampled copy)
+            g1 = ins.view(o1)[..., o1co:o1co + cout]
+            for dy in ((0, 1) if up1 else (0,)):
+                for dx in ((0, 1) if up1 else (0,)):
+                    part = g1[:, dy::2, dx::2] if up1 else g1
+                    np.testing.assert_array_equal(part, got, err_msg=name)
+    print("worst layers:", sorted(worst)[-3:])
+
+
+def test_first_conv_sppf_and_decode(cuda):
+    H, W, B = 1080, 1920, 1
+    eng, ins, specs, params, lb, raw = _setup(cuda, H, W, B)
+    # model.0: 3->16 k3 s2 from the u8 letterbox, f32 math
+    w, b = params["model.0"]
+    x = torch.from_numpy(lb[..., ::-1].transpose(0, 3, 1, 2).copy()).double() / 255
+    y = F.silu(F.conv2d(x, torch.from_numpy(w).double(), torch.from_numpy(b).double(), stride=2,
+                        padding=1)).numpy().transpose(0, 2, 3, 1)
+    got = ins.view(0)
+    d = np.abs(got - y)
+    assert (d <= ulp_bf16(y) * 1.01 + 1e-6).mean() > 0.9999 and (d <= 2 * ulp_bf16(y) + 1e-5).all()
+    # SPPF: channels [c,2c,3c,4c) are 5/9/13 max pools of [0,c) (exact)
+    sp = [i for i, bb in enumerate(ins.bufs) if bb[2] == 4 * (256 // 2) and bb[0] == 384 // 32]
+    assert sp, "SPPF buffer not found"
+    s = ins.view(sp[0])
+    c = s.shape[-1] // 4
+    t = torch.from_numpy(np.ascontiguousarray(s[..., :c].transpose(0, 3, 1, 2)))
+    p1 = F.max_pool2d(t, 5, 1, 2)
+    p2 = F.max_pool2d(p1, 5, 1, 2)
+    p3 = F.max_pool2d(p2, 5, 1, 2)
+    for j, p in enumerate((p1, p2, p3)):
+        np.testing.assert_array_equal(s[..., (j + 1) * c:(j + 2) * c], p.numpy().transpose(0, 2, 3, 1))
+    # decode from the GPU's own head logits
+    heads = [i for i, bb in enumerate(ins.bufs) if bb[3] == 1]
+    assert len(heads) == 3
+    outs, anc, st = [], [], []
+    for lvl, hb in enumerate(heads):
+        v = ins.view(hb)  # (B, h, w, 144)
+        h, w = v.shape[1:3]
+        outs.append(v.reshape(B, h * w, -1).transpose(0, 2, 1))
+        sy, sx = np.meshgrid(np.arange(h) + 0.5, np.arange(w) + 0.5, indexing="ij")
+        anc.append(np.stack([sx.ravel(), sy.ravel()]))
+        st.append(np.full(h * w, 8.0 * 2 ** lvl))
+    y = np.concatenate(outs, 2).astype(np.float64)
+    A = y.shape[2]
+    box = y[:, :64].reshape(B, 4, 16, A)
+    e = np.exp(box - box.max(2, keepdims=True))
+    dist = (e / e.sum(2, keepdims=True) * np.arange(16).reshape(1, 1, 16, 1)).sum(2)
+    an = np.concatenate(anc, 1)[None]
+    s_ = np.concatenate(st)[None]
+    x1y1, x2y2 = an - dist[:, :2], an + dist[:, 2:]
+    xywh = np.concatenate([(x1y1 + x2y2) / 2, x2y2 - x1y1], 1) * s_[:, None]
+    np.testing.assert_allclose(raw[:, :4], xywh, rtol=0, atol=2e-3)
+    np.testing.assert_allclose(raw[:, 4:], 1 / (1 + np.exp(-y[:, 64:])), rtol=0, atol=1e-6)
+    # candidates: every anchor with best score > conf, none else
+    n = int(eng.cand_n[0])
+    expect = int((raw[0, 4:].max(0) > 0.25).sum())
+    assert n == expect
