@@ -136,6 +136,14 @@ int rv_yolo_num_buffers(void* handle);
 int rv_yolo_buffer_info(void* handle, int B, int buf, int* info, size_t* off_bytes);
 int rv_yolo_trace(void* handle, int* recs, int max_recs);
 
+/* Live device timing of the conv launches (HIP events recorded on the launch
+ * stream around every conv_mfma launch of the next max_forwards forwards;
+ * 0 disables).  rv_yolo_profile_read synchronises on the events and returns,
+ * per conv launch index, the summed ms over the recorded forwards, the
+ * algorithmic FLOPs of one launch (2*M*N*K) and the conv index. */
+int rv_yolo_profile(void* handle, int max_forwards);
+int rv_yolo_profile_read(void* handle, double* ms, double* flops, int* conv, int n);
+
 /* --- Ultralytics non_max_suppression + scale_boxes + class filter
  * (yolo_ultralytics.py:28-53), one workgroup per image. */
 size_t rv_nms_smem_bytes(void);

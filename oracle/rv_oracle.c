@@ -167,7 +167,38 @@ void oracle_clahe_ycrcb(const uint8_t* in, uint8_t* out, int H, int W, int tiles
 
 /* cv::medianBlur 8UC3, odd k, BORDER_REPLICATE (exact median: partial
  * insertion sort of the k*k window). */
+static int min2(int a, int b) { return a < b ? a : b; }
+static int max2(int a, int b) { return a > b ? a : b; }
+static int med3(int a, int b, int c) { return max2(min2(a, b), min2(max2(a, b), c)); }
+
+/* k = 3 fast path: sort each column of 3, median = med3(max(lo), med(mid), min(hi)). */
+static void median3(const uint8_t* in, uint8_t* out, int H, int W) {
+  for (int y = 0; y < H; ++y) {
+    const uint8_t* r0 = in + (size_t)clampi(y - 1, 0, H - 1) * W * 3;
+    const uint8_t* r1 = in + (size_t)y * W * 3;
+    const uint8_t* r2 = in + (size_t)clampi(y + 1, 0, H - 1) * W * 3;
+    for (int x = 0; x < W; ++x)
+      for (int c = 0; c < 3; ++c) {
+        int lo[3], mi[3], hi[3];
+        for (int j = 0; j < 3; ++j) {
+          const int xx = clampi(x - 1 + j, 0, W - 1) * 3 + c;
+          const int a = r0[xx], b = r1[xx], d = r2[xx];
+          lo[j] = min2(min2(a, b), d);
+          hi[j] = max2(max2(a, b), d);
+          mi[j] = med3(a, b, d);
+        }
+        out[((size_t)y * W + x) * 3 + c] = (uint8_t)med3(max2(max2(lo[0], lo[1]), lo[2]),
+                                                         med3(mi[0], mi[1], mi[2]),
+                                                         min2(min2(hi[0], hi[1]), hi[2]));
+      }
+  }
+}
+
 void oracle_median_u8c3(const uint8_t* in, uint8_t* out, int H, int W, int k) {
+  if (k == 3) {
+    median3(in, out, H, W);
+    return;
+  }
   const int r = k / 2, n = k * k, rank = n / 2;
   int w[81];
   for (int y = 0; y < H; ++y)

@@ -245,8 +245,13 @@ extern "C" int rv_nms_postprocess(const void* cand, const int* cand_n, int B, in
   const size_t smem = rv_nms_smem_bytes();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)smem);
+    hipError_t e = hipFuncSetAttribute((const void*)nms_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) {
+      set_error("hipFuncSetAttribute(%zu B LDS): %s", smem, hipGetErrorString(e));
+      (void)hipGetLastError();
+      return -(int)e;
+    }
     attr = true;
   }
   nms_kernel<<<B, 1024, smem, as_stream(stream)>>>((const Cand*)cand, cand_n, cap, max_wh,

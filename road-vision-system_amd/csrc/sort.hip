@@ -578,8 +578,17 @@ extern "C" int rv_sort_update(void* state_in, void* state_out, int S, int tmax,
   Track* tout = (Track*)((uint8_t*)state_out + hb);
   const size_t smem = sort_smem(tmax, dmax);
   RV_CHECK_ARG(smem <= 160 * 1024, "tmax/dmax need %zu B of LDS", smem);
-  hipFuncSetAttribute((const void*)sort_update_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                      (int)smem);
+  static int attr_set = 0;
+  if ((int)smem > attr_set) {  // once per growth, outside steady-state launches
+    hipError_t e = hipFuncSetAttribute((const void*)sort_update_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) {
+      set_error("hipFuncSetAttribute(%zu B LDS): %s", smem, hipGetErrorString(e));
+      (void)hipGetLastError();
+      return -(int)e;
+    }
+    attr_set = (int)smem;
+  }
   sort_update_kernel<<<S, 256, smem, as_stream(stream)>>>(hin, tin, hout, tout, dets, dcount, ts, p,
                                                           (float*)ws, out_id, out_dist, out_speed);
   return launch_status("rv_sort_update");

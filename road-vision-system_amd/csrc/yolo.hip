@@ -176,8 +176,19 @@ struct TraceRec {
   int res_buf, res_cs, res_co, pad;
 };
 
+// Live per-launch timing of conv_mfma (bench roofline): one hipEvent pair
+// per conv launch per forward, recorded on the launch stream.
+struct Profile {
+  bool on = false;
+  int cap_fwd = 0, n_fwd = 0, per_fwd = 0;
+  std::vector<hipEvent_t> ev;     // [cap_fwd][per_fwd][2]
+  std::vector<double> flops;      // per conv launch index (algorithmic, 2*M*N*K)
+  std::vector<int> conv_of;       // conv spec index per launch index
+};
+
 struct Model {
   ModelDef def;
+  Profile prof;
   std::vector<TraceRec> trace;  // conv launches of the last forward
   std::vector<std::pair<std::string, int>> tmps;  // bottleneck temp buffer per "prefix.m.i"
   int tmp_of(const std::string& k) const {
@@ -344,8 +355,17 @@ struct Exec {
     r.res_buf = res.buf;
     r.res_cs = res.cs;
     r.res_co = res.co;
+    const int li_ = (int)M->trace.size();
     M->trace.push_back(r);
+    Profile& P = M->prof;
+    const bool rec = P.on && P.n_fwd < P.cap_fwd && li_ < P.per_fwd;
+    if (rec) hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + li_) * 2], s);
     status = launch_conv(a, s);
+    if (rec) hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + li_) * 2 + 1], s);
+    if (P.on && P.n_fwd == 0 && li_ < P.per_fwd) {
+      P.flops[li_] = 2.0 * B * a.Ho * a.Wo * (double)c.cout * c.cin * c.k * c.k;
+      P.conv_of[li_] = idx;
+    }
   }
 
   // C2f(prefix): in view (map li) -> concat buffer cb -> outputs
@@ -547,6 +567,7 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
     E.conv(c + ".2", View{M->DB[i], dcs, v.c2d}, 3 + i, View{M->HD[i], hcs, 4 * v.reg});
   }
   if (E.status) return E.status;
+  if (M->prof.on && M->prof.n_fwd < M->prof.cap_fwd) M->prof.n_fwd++;
   HeadLevel hl[3];
   for (int i = 0; i < 3; ++i) {
     hl[i].logits = (const float*)E.ptr(M->HD[i]);
@@ -585,4 +606,52 @@ extern "C" int rv_yolo_trace(void* h, int* recs, int max_recs) {
   if (recs)
     for (int i = 0; i < n && i < max_recs; ++i) memcpy(recs + 20 * i, &M->trace[i], 20 * sizeof(int));
   return n;
+}
+
+// ---- live conv timing ------------------------------------------------------
+extern "C" int rv_yolo_profile(void* h, int max_forwards) {
+  RV_CHECK_ARG(h && max_forwards >= 0, "bad args");
+  Model* M = (Model*)h;
+  Profile& P = M->prof;
+  for (hipEvent_t e : P.ev) hipEventDestroy(e);
+  P.ev.clear();
+  P.on = max_forwards > 0;
+  P.n_fwd = 0;
+  P.cap_fwd = max_forwards;
+  P.per_fwd = (int)M->def.convs.size();
+  P.flops.assign(P.per_fwd, 0.0);
+  P.conv_of.assign(P.per_fwd, -1);
+  if (!P.on) return RV_OK;
+  P.ev.resize((size_t)P.cap_fwd * P.per_fwd * 2);
+  for (auto& e : P.ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      set_error("hipEventCreate failed");
+      return RV_EINVAL;
+    }
+  return RV_OK;
+}
+
+// After the profiled forwards (synchronises): per conv launch index i,
+// ms[i] = total device time over the recorded forwards, flops[i] =
+// algorithmic FLOPs of ONE launch, conv[i] = conv spec index.  Returns the
+// number of recorded forwards.
+extern "C" int rv_yolo_profile_read(void* h, double* ms, double* flops, int* conv, int n) {
+  RV_CHECK_ARG(h && ms && flops && conv, "bad args");
+  Model* M = (Model*)h;
+  Profile& P = M->prof;
+  if (!P.on) return 0;
+  for (int i = 0; i < n && i < P.per_fwd; ++i) {
+    double tot = 0.0;
+    for (int f = 0; f < P.n_fwd; ++f) {
+      float t = 0.f;
+      hipEvent_t a = P.ev[((size_t)f * P.per_fwd + i) * 2], b = P.ev[((size_t)f * P.per_fwd + i) * 2 + 1];
+      if (P.conv_of[i] >= 0 && hipEventSynchronize(b) == hipSuccess &&
+          hipEventElapsedTime(&t, a, b) == hipSuccess)
+        tot += t;
+    }
+    ms[i] = tot;
+    flops[i] = P.flops[i];
+    conv[i] = P.conv_of[i];
+  }
+  return P.n_fwd;
 }
