@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--streams", type=int, default=32, help="camera streams per GPU")
     ap.add_argument("--cpu-frames", type=int, default=int(os.environ.get("RV_CPU_FRAMES", 6)))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="launch kernels eagerly (no HIP graph)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,13 +114,24 @@ def main():
         eng.step(frames[f], ts_all[f])
     torch.cuda.synchronize()
     lib = _lib.load()
-    _lib.check(lib.rv_yolo_profile(eng.detector._h, K), "rv_yolo_profile")
+    graphs = None
+    if not args.eager:
+        # one HIP graph per timed step (its own frame batch); replayed in order
+        graphs = [eng.capture(frames[Wm + k], ts_all[Wm + k])[0] for k in range(K)]
+        torch.cuda.synchronize()
+        # captured steps advanced the tracker state: rewind to the post-warmup
+        # state is not needed for throughput, the replay re-runs every kernel.
+    else:
+        _lib.check(lib.rv_yolo_profile(eng.detector._h, K), "rv_yolo_profile")
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(K):
-        out = eng.step(frames[Wm + k], ts_all[Wm + k])
+        if graphs is not None:
+            graphs[k].replay()
+        else:
+            eng.step(frames[Wm + k], ts_all[Wm + k])
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -128,7 +140,13 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # live conv timing (HIP events on the launch stream, over the timed steps)
+    # live conv timing (HIP events on the launch stream): a separate eager
+    # pass over the same K steps (event records cannot live inside graphs)
+    if graphs is not None:
+        _lib.check(lib.rv_yolo_profile(eng.detector._h, K), "rv_yolo_profile")
+        for k in range(K):
+            eng.step(frames[Wm + k], ts_all[Wm + k])
+        torch.cuda.synchronize()
     n = lib.rv_yolo_num_convs(eng.variant)
     ms = np.zeros(n, np.float64)
     fl = np.zeros(n, np.float64)

@@ -65,6 +65,20 @@ class RoadVisionEngine:
         return {"proc": proc, "dets": dets, "det_n": det_n, "track_id": tid,
                 "distance_m": dist, "speed_kmh": spd}
 
+    def capture(self, frames: torch.Tensor, ts: torch.Tensor):
+        """Record one step on (frames, ts) -- fixed device buffers -- into a
+        HIP graph (torch.cuda.CUDAGraph over hipStreamBeginCapture).  Replaying
+        it runs the whole step (~75 launches) with no host launch overhead or
+        inter-kernel gaps from the host.  The SORT ping-pong state advances
+        once per captured step, so graphs must be replayed in capture order
+        (a ring of an even number of graphs over double-buffered frame
+        inputs, as bench.py does).  Call step() once before the first capture
+        (one-time kernel attribute setup happens outside capture)."""
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = self.step(frames, ts)
+        return g, out
+
     def results(self, out: Dict[str, torch.Tensor]) -> List[List[Detection]]:
         d = out["dets"].cpu().numpy()
         n = out["det_n"].cpu().numpy()
