@@ -77,6 +77,24 @@ int rv_clahe_median_u8(const uint8_t* in, uint8_t* out, int B, int H, int W,
  * output tile fits in LDS), 0 if the caller must use the unfused pair. */
 int rv_clahe_median_fits(int H, int W, int tiles, int k);
 
+/* The default chain plus the detector's LetterBox in one pass:
+ * rv_clahe_median_u8 (k = 3) writing `out`, and the Ultralytics letterbox of
+ * `out` (geo from rv_letterbox_geometry) into lb_out (B x geo[0] x geo[1] x 3),
+ * byte-identical to rv_clahe_median_u8 followed by rv_letterbox_u8.  Replaces
+ * the pipeline -> detector hand-over of main_preview.py:99-101
+ * (PreprocessPipeline.__call__ then YOLOUltralytics.infer's LetterBox,
+ * src/detect/yolo_ultralytics.py:28-35).  RV_EINVAL unless
+ * rv_clahe_median_letterbox_fits() says 1. */
+int rv_clahe_median_letterbox_u8(const uint8_t* in, uint8_t* out, int B, int H, int W,
+                                 int pitch, int tiles, double clip, int k, void* ws,
+                                 size_t ws_bytes, uint8_t* lb_out, const int* geo,
+                                 void* stream);
+
+/* 1 if rv_clahe_median_letterbox_u8 supports this geometry: k = 3, the LUT
+ * cells of a 128 x 32 tile fit in LDS and every letterbox pixel's bilinear
+ * taps fall in one tile. */
+int rv_clahe_median_letterbox_fits(int H, int W, int tiles, int k, const int* geo);
+
 /* Low-contrast auto gate (src/preprocess/pipeline.py:24-30): per frame,
  * span_out[b] = max(gray) - min(gray), gray = cv2.COLOR_BGR2GRAY (14-bit
  * fixed point).  ws: 2*B ints of device scratch. */

@@ -30,7 +30,6 @@ struct ConvArgs {
   const bf16_t* res;
   int res_cs, res_co;
   int act;  // 1: SiLU
-  int dbg;  // ablation bits for experiments (0 in production)
 };
 
 // Implicit-GEMM conv on MFMA (v_mfma_f32_16x16x32_bf16).

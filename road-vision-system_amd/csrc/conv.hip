@@ -23,14 +23,22 @@ namespace rv {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+typedef __attribute__((ext_vector_type(2))) float f32x2v;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
+
+// f32 -> bf16, round to nearest even, on the hardware converter
+// (v_cvt_pk_bf16_f32: two values per instruction).
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{lo, hi}, bf16x2v));
 }
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 
-__device__ __forceinline__ float silu(float v) { return v / (1.0f + __expf(-v)); }
+// SiLU x * sigmoid(x) = x * 1/(1 + e^-x) with the hardware reciprocal
+// (<= 1 ulp f32; the result is stored as bf16).
+__device__ __forceinline__ float silu(float v) {
+  return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+}
 
 // Wave tile: MR x NR fragments of 16x16 (16*MR output channels x 16*NR
 // pixels).  A workgroup is 4 waves arranged WP (pixel groups) x WC (channel
@@ -179,8 +187,7 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
           }
         } else {
           uint16_t* o = (uint16_t*)outp;
-          const uint2 pk = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
-                                      (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+          const uint2 pk = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
           if (!up) {
             *(uint2*)(o + opix * cs_ + co_) = pk;
           } else {
@@ -270,9 +277,9 @@ __device__ __attribute__((aligned(64))) uint4 g_zero16[4];
 struct PatchGeo {
   int C, R;        // output tile cols / rows (R*C <= 64*NR)
   int PH, PW;      // input patch rows / cols
-  int npix16;      // DMA instructions for the patch (16 pixels each)
+  int pinst;       // DMA instructions for the patch (64 x 16-B slots each)
   int tiles_x, tiles_y;
-  int p_bytes;     // npix16 * 1024
+  int p_bytes;     // pinst * 1024
 };
 
 __device__ __forceinline__ int swz(int i) { return (i >> 2) & 3; }
@@ -328,8 +335,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[MR][NR]
           }
         } else {
           uint16_t* o = (uint16_t*)outp;
-          const uint2 pk = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
-                                      (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+          const uint2 pk = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
           if (!up) {
             *(uint2*)(o + opix * cs_ + co_) = pk;
           } else {
@@ -345,80 +351,133 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[MR][NR]
   }
 }
 
+// Patch layout in LDS: pixel pp of the halo patch owns 80 bytes at pp * 80
+// (its 32 channels = 4 x 16-B quarters + one 16-B pad slot).  The 80-B
+// stride makes the 16 pixels of a B fragment hit 16 disjoint 4-bank groups
+// (20 dwords apart), so a fragment read needs no swizzle and every tap's
+// address is the pixel's base plus a compile-time/uniform offset.  The DMA
+// stays lane-linear: lane l of DMA instruction j fills slot L = 64 j + l,
+// i.e. pixel L / 5, quarter L % 5 (quarter 4 = pad, fetched from the zero
+// block).
+constexpr int kPixB = 80;
+
+// Per-lane DMA source offsets of one patch (elements from the image base,
+// -1 = zero block), at most patch_maxit(NR, S) DMA instructions per wave.
+template <int NR, int S>
+constexpr int patch_maxit() {
+  return (S == 2 ? 6 : 3) * NR + 2;
+}
+
+// Persistent, software-pipelined form: the block owns cout tile blockIdx.y
+// and walks pixel tiles blockIdx.x, +gridDim.x, ...; the (tile, chunk)
+// steps are flattened so the DMA of step s+1 -- the next chunk or the next
+// tile's first chunk -- streams in while step s runs on MFMA and while the
+// previous tile's epilogue stores drain.  Per-lane DMA offsets are computed
+// once per tile (no integer division in the chunk loop).
 template <int MR, int NR, int K, int S>
-__global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a, PatchGeo g) {
+__global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int T2 = K * K;
   constexpr int BC = 16 * MR;
   constexpr int W_BYTES = BC * T2 * 64;
+  constexpr int MAXP = patch_maxit<NR, S>();
+  static_assert(MAXP <= 32, "tail mask is 32 bits");
+  constexpr int WJ = BC * T2 / 16;            // weight DMA instructions per chunk
+  constexpr int MAXW = (WJ + 3) / 4;
   const int stage_bytes = g.p_bytes + W_BYTES;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int col = lane & 15, quad = lane >> 4;
-  int bid = blockIdx.x;
-  const int tx = bid % g.tiles_x;
-  bid /= g.tiles_x;
-  const int ty = bid % g.tiles_y;
-  const int b = bid / g.tiles_y;
-  const int x0 = tx * g.C, y0 = ty * g.R;
   const int cout0 = blockIdx.y * BC;
   const int cout_pad = (a.Cout + 15) & ~15;
   const int cin_pad = (a.Cin + 31) & ~31;
   const int Kp = T2 * cin_pad;
   const int nch = cin_pad >> 5;
-  const int pad = K / 2;
+  constexpr int pad = K / 2;
+  const int tiles_img = g.tiles_x * g.tiles_y;
+  const int ntiles = a.B * tiles_img;
+  const int my_tiles = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int nsteps = my_tiles * nch;
+  const int npp = g.PH * g.PW;
+  const float inv_pw = 1.0f / (float)g.PW;
 
-  bool pv[NR];
-  int pbase[NR], pbv[NR], pyv[NR], pxv[NR];
+  // block-constant: output slots -> (r, cc) of the tile, patch byte base
+  int orow[NR], ocol[NR], pb80[NR];
+  bool oin[NR];
 #pragma unroll
   for (int n = 0; n < NR; ++n) {
     const int q = wave * (NR * 16) + n * 16 + col;
-    const int r = q / g.C, cc = q - (q / g.C) * g.C;
-    pv[n] = q < g.R * g.C && y0 + r < a.Ho && x0 + cc < a.Wo;
-    pbase[n] = pv[n] ? (r * S) * g.PW + cc * S : 0;
-    pbv[n] = b;
-    pyv[n] = y0 + r;
-    pxv[n] = x0 + cc;
+    orow[n] = q / g.C;
+    ocol[n] = q - orow[n] * g.C;
+    oin[n] = q < g.R * g.C;
+    pb80[n] = (oin[n] ? (orow[n] * S) * g.PW + ocol[n] * S : 0) * kPixB + quad * 16;
   }
-  f32x4 acc[MR][NR];
+  // block-constant: weight DMA offsets (chunk 0) per instruction
+  int woff[MAXW];
 #pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int it = 0; it < MAXW; ++it) {
+    const int j = wave + 4 * it;
+    const int pr = j * 16 + (lane >> 2);
+    const int row = pr / T2, tap = pr - (pr / T2) * T2;
+    const int q = (lane & 3) ^ swz(row);
+    const int co = cout0 + row;
+    woff[it] = (j < WJ && co < cout_pad) ? co * Kp + tap * cin_pad + q * 8 : -1;
+  }
 
-  const int npp = g.PH * g.PW;
-  const bf16_t* img = a.in + (size_t)b * a.Hin * a.Win * a.in_cs + a.in_co;
+  int poff[MAXP];
+  uint32_t tailbad = 0;  // bit it: this lane's quarter is >= Cin in the last chunk
+  const bf16_t* img = a.in;
+  auto prep_tile = [&](int ti) {
+    const int b = ti / tiles_img;
+    const int r = ti - b * tiles_img;
+    const int ty = r / g.tiles_x, tx = r - (r / g.tiles_x) * g.tiles_x;
+    const int iy0 = ty * g.R * S - pad, ix0 = tx * g.C * S - pad;
+    img = a.in + (size_t)b * a.Hin * a.Win * a.in_cs + a.in_co;
+    tailbad = 0;
+#pragma unroll
+    for (int it = 0; it < MAXP; ++it) {
+      const int L = 64 * (wave + 4 * it) + lane;
+      const int pix = L / 5, q = L - 5 * pix;
+      const int py = (int)(((float)pix + 0.5f) * inv_pw);
+      const int px = pix - py * g.PW;
+      const int iy = iy0 + py, ix = ix0 + px;
+      const bool ok = q < 4 && pix < npp && (unsigned)iy < (unsigned)a.Hin &&
+                      (unsigned)ix < (unsigned)a.Win;
+      poff[it] = ok ? (iy * a.Win + ix) * a.in_cs + q * 8 : -1;
+      if ((nch - 1) * 32 + q * 8 >= a.Cin) tailbad |= 1u << it;
+    }
+  };
   auto stage = [&](int c, int buf) {
     uint8_t* P = smem + buf * stage_bytes;
     uint8_t* Wl = P + g.p_bytes;
-    const int slot = lane & 3;
-    for (int j = wave; j < g.npix16; j += 4) {
-      const int pp = j * 16 + (lane >> 2);
-      const int q = slot ^ swz(pp);
-      const int py = pp / g.PW, px = pp - (pp / g.PW) * g.PW;
-      const int iy = y0 * S - pad + py, ix = x0 * S - pad + px;
-      const bool ok = pp < npp && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win &&
-                      c * 32 + q * 8 < a.Cin;
-      const void* src = ok ? (const void*)(img + ((size_t)iy * a.Win + ix) * a.in_cs + c * 32 + q * 8)
-                           : (const void*)g_zero16;
-      __builtin_amdgcn_global_load_lds(src, (void*)(P + j * 1024), 16, 0, 0);
+    const uint32_t bad = c == nch - 1 ? tailbad : 0u;
+#pragma unroll
+    for (int it = 0; it < MAXP; ++it) {
+      const int j = wave + 4 * it;
+      if (j < g.pinst) {
+        const void* src = (poff[it] >= 0 && !((bad >> it) & 1))
+                              ? (const void*)(img + poff[it] + c * 32)
+                              : (const void*)g_zero16;
+        __builtin_amdgcn_global_load_lds(src, (void*)(P + j * 1024), 16, 0, 0);
+      }
     }
-    for (int j = wave; j < BC * T2 / 16; j += 4) {
-      const int pr = j * 16 + (lane >> 2);
-      const int row = pr / T2, tap = pr - (pr / T2) * T2;
-      const int q = slot ^ swz(row);
-      const int co = cout0 + row;
-      const void* src = co < cout_pad
-                            ? (const void*)(a.w + (size_t)co * Kp + tap * cin_pad + c * 32 + q * 8)
-                            : (const void*)g_zero16;
-      __builtin_amdgcn_global_load_lds(src, (void*)(Wl + j * 1024), 16, 0, 0);
+#pragma unroll
+    for (int it = 0; it < MAXW; ++it) {
+      const int j = wave + 4 * it;
+      if (j < WJ) {
+        const void* src = woff[it] >= 0 ? (const void*)(a.w + woff[it] + c * 32)
+                                        : (const void*)g_zero16;
+        __builtin_amdgcn_global_load_lds(src, (void*)(Wl + j * 1024), 16, 0, 0);
+      }
     }
   };
+  f32x4 acc[MR][NR];
   auto compute = [&](int buf) {
     const uint8_t* P = smem + buf * stage_bytes;
     const uint8_t* Wl = P + g.p_bytes;
 #pragma unroll
-    for (int ky = 0; ky < K; ++ky)
+    for (int ky = 0; ky < K; ++ky) {
+      const uint8_t* Prow = P + ky * g.PW * kPixB;
 #pragma unroll
       for (int kx = 0; kx < K; ++kx) {
         const int tap = ky * K + kx;
@@ -430,25 +489,58 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a, PatchGeo g)
               bf16x8, *(const uint4*)(Wl + (row * T2 + tap) * 64 + ((quad ^ swz(row)) << 4)));
         }
 #pragma unroll
-        for (int n = 0; n < NR; ++n) {
-          const int pp = pbase[n] + ky * g.PW + kx;
-          Bf[n] = __builtin_bit_cast(bf16x8, *(const uint4*)(P + pp * 64 + ((quad ^ swz(pp)) << 4)));
-        }
+        for (int n = 0; n < NR; ++n)
+          Bf[n] = __builtin_bit_cast(bf16x8, *(const uint4*)(Prow + pb80[n] + kx * kPixB));
 #pragma unroll
         for (int m = 0; m < MR; ++m)
 #pragma unroll
           for (int n = 0; n < NR; ++n)
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[m], Bf[n], acc[m][n], 0, 0, 0);
       }
+    }
   };
+
+  if (nsteps == 0) return;
+  int ti = blockIdx.x;  // tile of the current step
+  int c = 0;            // chunk of the current step
+  prep_tile(ti);
   stage(0, 0);
   __syncthreads();
-  for (int c = 0; c < nch; ++c) {
-    if (c + 1 < nch && !(a.dbg & 2)) stage(c + 1, (c + 1) & 1);
-    if (!(a.dbg & 1)) compute(c & 1);
+  for (int s = 0; s < nsteps; ++s) {
+    if (c == 0) {
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // issue step s+1
+    const bool last = c + 1 == nch;
+    if (s + 1 < nsteps) {
+      if (last) prep_tile(ti + gridDim.x);
+      stage(last ? 0 : c + 1, (s + 1) & 1);
+    }
+    compute(s & 1);
+    if (last) {
+      const int b = ti / tiles_img;
+      const int r = ti - b * tiles_img;
+      const int ty = r / g.tiles_x, tx = r - (r / g.tiles_x) * g.tiles_x;
+      bool pv[NR];
+      int pb[NR], py[NR], px[NR];
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        pb[n] = b;
+        py[n] = ty * g.R + orow[n];
+        px[n] = tx * g.C + ocol[n];
+        pv[n] = oin[n] && py[n] < a.Ho && px[n] < a.Wo;
+      }
+      epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad);
+      ti += gridDim.x;
+      c = 0;
+    } else {
+      ++c;
+    }
     __syncthreads();
   }
-  epilogue<MR, NR>(a, acc, cout0, pv, pbv, pyv, pxv, quad);
 }
 
 static bool patch_geo(const ConvArgs& a, int NR, int MR, PatchGeo& g, size_t& smem) {
@@ -471,14 +563,30 @@ static bool patch_geo(const ConvArgs& a, int NR, int MR, PatchGeo& g, size_t& sm
   if (g.R < 1) return false;
   g.PH = (g.R - 1) * a.stride + a.k;
   g.PW = (g.C - 1) * a.stride + a.k;
-  g.npix16 = (g.PH * g.PW + 15) / 16;
-  g.p_bytes = g.npix16 * 1024;
+  g.pinst = ceil_div(g.PH * g.PW * 5, 64);  // 5 x 16-B slots per pixel (kPixB)
+  g.p_bytes = g.pinst * 1024;
   g.tiles_x = ceil_div(a.Wo, g.C);
   g.tiles_y = ceil_div(a.Ho, g.R);
-  const int nch = ((a.Cin + 31) & ~31) / 32;
-  // double-buffer only when there is a next chunk to overlap
-  smem = (nch > 1 ? 2 : 1) * ((size_t)g.p_bytes + (size_t)16 * MR * a.k * a.k * 64);
+  // per-lane offset registers of the kernel (patch_maxit)
+  const int maxit = (a.stride == 2 ? 6 : 3) * NR + 2;
+  if (ceil_div(g.pinst, 4) > maxit) return false;
+  // two stages: the next (tile, chunk) streams in during the current one
+  smem = 2 * ((size_t)g.p_bytes + (size_t)16 * MR * a.k * a.k * 64);
   return smem <= 160 * 1024;
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess)
+      n = p.multiProcessorCount;
+    else
+      n = 256;
+    (void)hipGetLastError();
+  }
+  return n;
 }
 
 template <int MR, int NR, int K, int S>
@@ -494,25 +602,57 @@ static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, hip
     }
     attr = true;
   }
+  // resident blocks per CU at this LDS size (cached per size)
+  static size_t occ_smem[8] = {0};
+  static int occ_val[8] = {0};
+  int occ = 0;
+  for (int i = 0; i < 8; ++i)
+    if (occ_smem[i] == smem) occ = occ_val[i];
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_patch_kernel<MR, NR, K, S>, 256,
+                                                     smem) != hipSuccess || occ < 1)
+      occ = 1;
+    (void)hipGetLastError();
+    for (int i = 0; i < 8; ++i)
+      if (occ_smem[i] == 0) {
+        occ_smem[i] = smem;
+        occ_val[i] = occ;
+        break;
+      }
+  }
+  static const int persist = getenv("RV_CONV_PERSIST") ? atoi(getenv("RV_CONV_PERSIST")) : 1;
   const int T = (a.Cout + 15) / 16;
-  dim3 grid(a.B * g.tiles_x * g.tiles_y, ceil_div(T, MR));
+  const int ytiles = ceil_div(T, MR);
+  const int ntiles = a.B * g.tiles_x * g.tiles_y;
+  int gx = ntiles;
+  if (persist) gx = std::min(ntiles, std::max(1, num_cus() * occ / ytiles));
+  dim3 grid(gx, ytiles);
   conv_patch_kernel<MR, NR, K, S><<<grid, 256, smem, s>>>(a, g);
   return launch_status("conv_patch");
+}
+
+// stride-2 patches are ~4x the tile: only tiles whose offset registers and
+// accumulators fit without spills (NR <= 2, MR * NR <= 8) are built for S = 2
+template <int MR, int NR>
+constexpr bool patch_s2_ok() {
+  return NR <= 2 && MR * NR <= 8;
 }
 
 template <int MR, int NR>
 static int launch_patch_ks(const ConvArgs& a, const PatchGeo& g, size_t smem, hipStream_t s) {
   if (a.k == 3 && a.stride == 1) return launch_patch_t<MR, NR, 3, 1>(a, g, smem, s);
-  if (a.k == 3 && a.stride == 2) return launch_patch_t<MR, NR, 3, 2>(a, g, smem, s);
   if (a.k == 1 && a.stride == 1) return launch_patch_t<MR, NR, 1, 1>(a, g, smem, s);
-  return launch_patch_t<MR, NR, 1, 2>(a, g, smem, s);
+  if constexpr (patch_s2_ok<MR, NR>()) {
+    if (a.k == 3) return launch_patch_t<MR, NR, 3, 2>(a, g, smem, s);
+    return launch_patch_t<MR, NR, 1, 2>(a, g, smem, s);
+  }
+  set_error("conv_patch: no stride-2 variant MR=%d NR=%d", MR, NR);
+  return RV_EINVAL;
 }
 
 // returns 1 if launched (status in *st), 0 if the patch kernel does not apply
 static int try_launch_patch(const ConvArgs& a_in, hipStream_t s, int* st) {
   ConvArgs a = a_in;
-  static const int ablate = getenv("RV_CONV_ABLATE") ? atoi(getenv("RV_CONV_ABLATE")) : 0;
-  a.dbg = ablate;
   static const char* force = getenv("RV_CONV_FORCE");  // "direct" or "MR,NR" (experiments)
   const int T = (a.Cout + 15) / 16;
   if (force && strcmp(force, "direct") == 0) return 0;
@@ -533,6 +673,7 @@ static int try_launch_patch(const ConvArgs& a_in, hipStream_t s, int* st) {
     if (c.mr > T && c.mr > 1) continue;
     if (ceil_div(T, c.mr) * c.mr - T > (c.mr > 1 ? 1 : 0)) continue;
     if (a.k == 3 && c.mr > 4) continue;  // keep 3x3 weight stages <= 37 KB
+    if (a.stride == 2 && (c.nr > 2 || c.mr * c.nr > 8)) continue;  // patch_s2_ok
     PatchGeo g;
     size_t sm;
     if (!patch_geo(a, c.nr, c.mr, g, sm)) continue;
@@ -573,83 +714,156 @@ static int try_launch_patch(const ConvArgs& a_in, hipStream_t s, int* st) {
 }
 
 // ---------------------------------------------------------------------------
-// conv0: 3 -> C0, k3 s2 p1, from letterboxed u8 BGR, f32 math, SiLU, bf16 out.
+// conv0: 3 -> C0, k3 s2 p1, from letterboxed u8 BGR, SiLU, bf16 out.
 // ---------------------------------------------------------------------------
-// One workgroup per 8 x 32 output tile: the (17 x 65) x 3 u8 input window
-// is staged in LDS as f32 (x / 255, RGB order) with coalesced byte loads,
-// then each thread computes all C0 channels of one output pixel.
-template <int C0>
+// conv0 on MFMA.  GEMM view: D[cout][px] = sum_k W'[cout][k] X[k][px] with
+// k = ky*9 + kx*3 + ch over the 3x3 window's 27 BGR bytes (padded to 32)
+// and X the raw u8 values, exact in bf16.  The 1/255 scale and the BGR->RGB
+// channel order live in W' = w[cout][2-ch][ky][kx] / 255, split into three
+// bf16 parts (hi + mid + lo, three MFMAs), so the products carry the f32
+// weight's full 24-bit significand and accumulate in f32.
+// Workgroup = 8 x 64 output pixels; wave w owns the 16-pixel-wide column
+// strip w and its 8 rows (one 16-pixel MFMA group per row).  The
+// (17 x 129) x 3 byte input window is staged in LDS as u16 (bf16 bit
+// patterns), so a lane's 8 k-values are 8 ds_read_u16 at per-lane addresses
+// fixed for the whole block plus a compile-time per-row offset.
+constexpr int kC0TH = 8, kC0TW = 64;
+constexpr int kC0IW = (2 * kC0TW + 1) * 3;  // 387 bytes per input row
+constexpr int kC0RS = kC0IW + 5;            // LDS row stride (u16 elements, 8-B multiple)
+
+template <int MR>
 __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ img, int B, int H,
                                                     int W, const float* __restrict__ w,
                                                     const float* __restrict__ bias,
                                                     uint16_t* __restrict__ out, int out_cs) {
-  constexpr int TH = 8, TW = 32, IH = 2 * TH + 1, IW = 2 * TW + 1;
-  __shared__ float ws[C0 * 27];
-  __shared__ float bs[C0];
-  __shared__ float xin[3][IH][IW + 1];
+  __shared__ uint16_t xin[(2 * kC0TH + 1) * kC0RS];
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
-  const int tiles_x = (Wo + TW - 1) / TW;
-  const int tiles_y = (Ho + TH - 1) / TH;
+  const int tiles_x = (Wo + kC0TW - 1) / kC0TW;
+  const int tiles_y = (Ho + kC0TH - 1) / kC0TH;
   int bid = blockIdx.x;
   const int tx = bid % tiles_x;
   bid /= tiles_x;
   const int ty = bid % tiles_y;
   const int b = bid / tiles_y;
-  const int oy0 = ty * TH, ox0 = tx * TW;
-  const int iy0 = oy0 * 2 - 1, ix0 = ox0 * 2 - 1;
-  for (int i = threadIdx.x; i < C0 * 27; i += 256) ws[i] = w[i];
-  for (int i = threadIdx.x; i < C0; i += 256) bs[i] = bias[i];
+  const int oy0 = ty * kC0TH, ox0 = tx * kC0TW;
+  const int iy0 = oy0 * 2 - 1, bx0 = (ox0 * 2 - 1) * 3;  // first input row / byte column
   const uint8_t* frame = img + (size_t)b * H * W * 3;
-  for (int i = threadIdx.x; i < IH * IW * 3; i += 256) {
-    const int r = i / (IW * 3);
-    const int rem = i - r * (IW * 3);
-    const int cx = rem / 3, ch = rem - (rem / 3) * 3;  // ch: BGR byte index
-    const int iy = iy0 + r, ix = ix0 + cx;
-    float v = 0.f;
-    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-      v = (float)frame[((size_t)iy * W + ix) * 3 + ch] / 255.0f;
-    xin[2 - ch][r][cx] = v;  // RGB plane order of the reference input
+  const int tid = threadIdx.x;
+  // Stage the window as bf16 bit patterns, element e = byte column e - 1
+  // (so dword-aligned source words land on dword-aligned LDS pairs): all
+  // dword loads of a thread are issued before any conversion.
+  constexpr int kDw = (kC0IW + 1 + 3) / 4;             // dwords per row (388 B)
+  constexpr int kN = (2 * kC0TH + 1) * kDw;            // 1649
+  constexpr int kIt = (kN + 255) / 256;                // 7
+  const bool aligned_rows = (W * 3) % 4 == 0 && ((uintptr_t)frame & 3) == 0;
+  uint32_t dv[kIt];
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int i = tid + it * 256;
+    dv[it] = 0;
+    if (i < kN) {
+      const int r = i / kDw, d = i - (i / kDw) * kDw;
+      const int iy = iy0 + r, a = bx0 - 1 + 4 * d;  // first byte of this word
+      if ((unsigned)iy < (unsigned)H) {
+        const uint8_t* row = frame + (size_t)iy * W * 3;
+        if (aligned_rows && a >= 0 && a + 3 < W * 3) {
+          dv[it] = *(const uint32_t*)(row + a);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (a + q >= 0 && a + q < W * 3) dv[it] |= (uint32_t)row[a + q] << (8 * q);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int i = tid + it * 256;
+    if (i < kN) {
+      const int r = i / kDw, d = i - (i / kDw) * kDw;
+      // bf16 of a byte value v is the high half of the f32 (float)v
+      const uint32_t f0 = __float_as_uint((float)(dv[it] & 255));
+      const uint32_t f1 = __float_as_uint((float)((dv[it] >> 8) & 255));
+      const uint32_t f2 = __float_as_uint((float)((dv[it] >> 16) & 255));
+      const uint32_t f3 = __float_as_uint((float)(dv[it] >> 24));
+      uint32_t* dst = (uint32_t*)(xin + r * kC0RS + 4 * d);
+      dst[0] = (f0 >> 16) | (f1 & 0xFFFF0000u);
+      dst[1] = (f2 >> 16) | (f3 & 0xFFFF0000u);
+    }
+  }
+  const int wave = tid >> 6, lane = tid & 63;
+  const int col = lane & 15, quad = lane >> 4;
+  // A fragments: rows cout = 16m + col, k = 8*quad + j
+  bf16x8 Ah[MR], Am[MR], Al[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    const int co = 16 * m + col;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * quad + j;
+      float v = 0.f;
+      if (k < 27) {
+        const int ky = k / 9, rem = k - ky * 9, kx = rem / 3, ch = rem - kx * 3;
+        v = w[((co * 3 + (2 - ch)) * 3 + ky) * 3 + kx] / 255.0f;
+      }
+      const __bf16 hi = (__bf16)v;
+      const float r1 = v - (float)hi;
+      const __bf16 mid = (__bf16)r1;
+      Ah[m][j] = hi;
+      Am[m][j] = mid;
+      Al[m][j] = (__bf16)(r1 - (float)mid);
+    }
+  }
+  float bv[MR][4];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[m][i] = bias[16 * m + 4 * quad + i];
+  // this lane's 8 k-value addresses for output pixel (row 0, x = 16*wave + col)
+  int koff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * quad + j;
+    const int kk = k < 27 ? k : 0;  // padded k: any value, its weight is 0
+    const int ky = kk / 9, rem = kk - ky * 9;
+    koff[j] = ky * kC0RS + (16 * wave + col) * 6 + rem + 1;  // element = byte column + 1
   }
   __syncthreads();
-  const int ly = threadIdx.x / TW, lx = threadIdx.x % TW;
-  const int oy = oy0 + ly, ox = ox0 + lx;
-  if (oy >= Ho || ox >= Wo) return;
-  float x[27];
 #pragma unroll
-  for (int ci = 0; ci < 3; ++ci)
+  for (int r = 0; r < kC0TH; ++r) {
+    const int oy = oy0 + r;
+    bf16x8 X;
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+    for (int j = 0; j < 8; ++j) X[j] = __builtin_bit_cast(__bf16, xin[koff[j] + 2 * r * kC0RS]);
+    f32x4 acc[MR];
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) x[ci * 9 + ky * 3 + kx] = xin[ci][2 * ly + ky][2 * lx + kx];
-  uint16_t* o = out + (((size_t)b * Ho + oy) * Wo + ox) * out_cs;
-#pragma unroll
-  for (int c8 = 0; c8 < C0; c8 += 8) {
-    uint32_t pk[4];
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      float v2[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int c = c8 + j + u;
-        float acc = 0.f;
-#pragma unroll
-        for (int t = 0; t < 27; ++t) acc += ws[c * 27 + t] * x[t];
-        v2[u] = silu(acc + bs[c]);
-      }
-      pk[j / 2] = (uint32_t)f2bf(v2[0]) | ((uint32_t)f2bf(v2[1]) << 16);
+    for (int m = 0; m < MR; ++m) {
+      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al[m], X, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am[m], X, acc[m], 0, 0, 0);
+      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[m], X, acc[m], 0, 0, 0);
     }
-    *(uint4*)(o + c8) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    const int ox = ox0 + 16 * wave + col;
+    if (oy < Ho && ox < Wo) {
+      uint16_t* o = out + (((size_t)b * Ho + oy) * Wo + ox) * out_cs;
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        const float v0 = silu(acc[m][0] + bv[m][0]), v1 = silu(acc[m][1] + bv[m][1]);
+        const float v2 = silu(acc[m][2] + bv[m][2]), v3 = silu(acc[m][3] + bv[m][3]);
+        *(uint2*)(o + 16 * m + 4 * quad) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+      }
+    }
   }
 }
 
 int launch_conv0(const uint8_t* img, int B, int H, int W, const float* w, const float* bias,
                  int C0, bf16_t* out, int out_cs, hipStream_t s) {
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
-  const int blocks = B * ceil_div(Ho, 8) * ceil_div(Wo, 32);
-  if (C0 == 16) conv0_kernel<16><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
-  else if (C0 == 32) conv0_kernel<32><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
-  else if (C0 == 48) conv0_kernel<48><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
-  else if (C0 == 64) conv0_kernel<64><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
+  const int blocks = B * ceil_div(Ho, kC0TH) * ceil_div(Wo, kC0TW);
+  if (C0 == 16) conv0_kernel<1><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
+  else if (C0 == 32) conv0_kernel<2><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
+  else if (C0 == 48) conv0_kernel<3><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
+  else if (C0 == 64) conv0_kernel<4><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
+  else if (C0 == 80) conv0_kernel<5><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
   else {
     set_error("conv0 C0=%d unsupported", C0);
     return RV_EINVAL;
@@ -661,64 +875,102 @@ int launch_conv0(const uint8_t* img, int B, int H, int W, const float* w, const 
 // SPPF: three chained MaxPool2d(5, 1, 2) == clipped 5/9/13 windows.
 // One thread per (pixel, 8-channel group).
 // ---------------------------------------------------------------------------
-// One workgroup per (image, 32-channel group): the H x W x 32 slice of x is
-// staged in LDS, every (pixel, 8-channel chunk) item then takes the clipped
-// 5/9/13 window maxima from LDS (bf16 max is exact).
-constexpr int kSppfLds = 64 * 1024;
+// One workgroup per (image, 8-channel group).  The clipped k x k max is
+// separable (the clipped window is a rectangle), so a horizontal pass writes
+// the row maxima for k = 5/9/13 to LDS and a vertical pass finishes them;
+// one thread per pixel, 8 channels (one 16-B vector) each.  bf16 max is
+// exact, so values stay bf16 throughout.
+constexpr int kSppfLds = 160 * 1024;
+
+__device__ __forceinline__ void bf8_to_f(const uint4 v, float (&f)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = __uint_as_float(w[j] << 16);
+    f[2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u);
+  }
+}
+__device__ __forceinline__ uint4 f_to_bf8(const float (&f)[8]) {
+  // inputs are bf16 values: truncation is exact
+  uint32_t w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    w[j] = (__float_as_uint(f[2 * j]) >> 16) | (__float_as_uint(f[2 * j + 1]) & 0xFFFF0000u);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
 
 __global__ __launch_bounds__(256) void sppf_pool_kernel(uint16_t* __restrict__ buf, int B, int H,
                                                         int W, int c) {
-  extern __shared__ __attribute__((aligned(16))) uint4 xs[];  // [H*W][4] (32 ch)
-  const int groups = c / 32;
-  const int b = blockIdx.x / groups, g = blockIdx.x % groups;
+  extern __shared__ __attribute__((aligned(16))) uint4 sp[];  // x, h5, h9, h13: [H*W] uint4 each
+  const int groups = c / 8;
+  const int b = blockIdx.x / groups, g = blockIdx.x - (blockIdx.x / groups) * groups;
   const int cs = 4 * c;
   const int HW = H * W;
-  uint16_t* img = buf + (size_t)b * HW * cs;
-  for (int i = threadIdx.x; i < HW * 4; i += 256) {
-    const int p = i >> 2, q = i & 3;
-    xs[i] = *(const uint4*)(img + (size_t)p * cs + g * 32 + q * 8);
-  }
+  uint4* xs = sp;
+  uint4* h5 = sp + HW;
+  uint4* h9 = sp + 2 * HW;
+  uint4* h13 = sp + 3 * HW;
+  uint16_t* img = buf + (size_t)b * HW * cs + g * 8;
+  for (int p = threadIdx.x; p < HW; p += 256) xs[p] = *(const uint4*)(img + (size_t)p * cs);
   __syncthreads();
-  for (int it = threadIdx.x; it < HW * 4; it += 256) {
-    const int p = it >> 2, q = it & 3;
+  for (int p = threadIdx.x; p < HW; p += 256) {
     const int y = p / W, x = p - (p / W) * W;
-    float m5[8], m9[8], m13[8];
+    float a5[8], a9[8], a13[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) m5[j] = m9[j] = m13[j] = -INFINITY;
-    const int y0 = max(y - 6, 0), y1 = min(y + 6, H - 1);
-    const int x0 = max(x - 6, 0), x1 = min(x + 6, W - 1);
-    for (int yy = y0; yy <= y1; ++yy) {
-      const int ady = yy < y ? y - yy : yy - y;
-      for (int xx = x0; xx <= x1; ++xx) {
-        const int adx = xx < x ? x - xx : xx - x;
-        const int rad = ady > adx ? ady : adx;
-        const uint4 v = xs[(yy * W + xx) * 4 + q];
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    for (int j = 0; j < 8; ++j) a5[j] = a9[j] = a13[j] = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float f = bf2f((uint16_t)(wv[j / 2] >> ((j & 1) * 16)));
-          m13[j] = fmaxf(m13[j], f);
-          if (rad <= 4) m9[j] = fmaxf(m9[j], f);
-          if (rad <= 2) m5[j] = fmaxf(m5[j], f);
-        }
+    for (int d = -6; d <= 6; ++d) {
+      const int xx = x + d;
+      if (xx < 0 || xx >= W) continue;
+      float f[8];
+      bf8_to_f(xs[y * W + xx], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a13[j] = fmaxf(a13[j], f[j]);
+        if (d >= -4 && d <= 4) a9[j] = fmaxf(a9[j], f[j]);
+        if (d >= -2 && d <= 2) a5[j] = fmaxf(a5[j], f[j]);
       }
     }
-    uint16_t* o = img + (size_t)p * cs + g * 32 + q * 8;
-    const float* src[3] = {m5, m9, m13};
+    h5[p] = f_to_bf8(a5);
+    h9[p] = f_to_bf8(a9);
+    h13[p] = f_to_bf8(a13);
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < HW; p += 256) {
+    const int y = p / W, x = p - (p / W) * W;
+    float a5[8], a9[8], a13[8];
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      uint32_t pk[4];
+    for (int j = 0; j < 8; ++j) a5[j] = a9[j] = a13[j] = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        pk[j] = (uint32_t)f2bf(src[s][2 * j]) | ((uint32_t)f2bf(src[s][2 * j + 1]) << 16);
-      *(uint4*)(o + (s + 1) * c) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    for (int d = -6; d <= 6; ++d) {
+      const int yy = y + d;
+      if (yy < 0 || yy >= H) continue;
+      const int q = yy * W + x;
+      float f[8];
+      bf8_to_f(h13[q], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a13[j] = fmaxf(a13[j], f[j]);
+      if (d >= -4 && d <= 4) {
+        bf8_to_f(h9[q], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a9[j] = fmaxf(a9[j], f[j]);
+      }
+      if (d >= -2 && d <= 2) {
+        bf8_to_f(h5[q], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a5[j] = fmaxf(a5[j], f[j]);
+      }
     }
+    uint16_t* o = img + (size_t)p * cs;
+    *(uint4*)(o + c) = f_to_bf8(a5);
+    *(uint4*)(o + 2 * c) = f_to_bf8(a9);
+    *(uint4*)(o + 3 * c) = f_to_bf8(a13);
   }
 }
 
 int launch_sppf_pool(bf16_t* buf, int B, int H, int W, int c, hipStream_t s) {
-  const size_t smem = (size_t)H * W * 64;
-  if (c % 32 != 0 || smem > kSppfLds) {
+  const size_t smem = (size_t)H * W * 64;  // 4 x 16 B per pixel
+  if (c % 8 != 0 || smem > kSppfLds) {
     set_error("sppf: c=%d / map %dx%d unsupported by the LDS pool", c, H, W);
     return RV_EINVAL;
   }
@@ -729,7 +981,7 @@ int launch_sppf_pool(bf16_t* buf, int B, int H, int W, int c, hipStream_t s) {
     (void)hipGetLastError();
     attr = true;
   }
-  sppf_pool_kernel<<<B * (c / 32), 256, smem, s>>>(buf, B, H, W, c);
+  sppf_pool_kernel<<<B * (c / 8), 256, smem, s>>>(buf, B, H, W, c);
   return launch_status("sppf_pool");
 }
 
@@ -744,15 +996,19 @@ struct HeadLevels {
   int nlv;
 };
 
-// One wave per 64 consecutive anchors of one level: their (64 x cs) f32
-// head logits are one contiguous span, staged into LDS with coalesced 16-B
-// loads; then each lane decodes its anchor from LDS.
+// One 256-thread workgroup per 64 consecutive anchors of one level: their
+// (64 x cs) f32 head logits are one contiguous span, staged into LDS with
+// coalesced 16-B loads at a padded row stride (cs + 4 floats: rows 20 banks
+// apart, conflict-free fragment reads).  Four lanes share an anchor: lane
+// part p takes the DFL side p (softmax expectation over REG bins) and the
+// classes p, p+4, ...; the quad then combines the four sides and the
+// first-max class with lane shuffles.
 template <int REG>
-__global__ __launch_bounds__(64) void detect_decode_kernel(HeadLevels h, int B, int nc,
-                                                           float conf, float* __restrict__ raw,
-                                                           Cand* __restrict__ cand, int cap,
-                                                           int* __restrict__ cand_n) {
-  extern __shared__ __attribute__((aligned(16))) float lg[];  // [64][cs]
+__global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B, int nc,
+                                                            float conf, float* __restrict__ raw,
+                                                            Cand* __restrict__ cand, int cap,
+                                                            int* __restrict__ cand_n) {
+  extern __shared__ __attribute__((aligned(16))) float lg[];  // [64][cs + 4]
   const int A = h.start[h.nlv];
   const int b = blockIdx.y;
   // block -> (level, first anchor in level)
@@ -762,24 +1018,39 @@ __global__ __launch_bounds__(64) void detect_decode_kernel(HeadLevels h, int B, 
   const int HW = L.H * L.W;
   const int r0 = (blk - h.blk[l]) * 64;
   const int na = min(64, HW - r0);
-  const int lane = threadIdx.x;
-  const float* src = L.logits + ((size_t)b * HW + r0) * L.cs;
-  const int n4 = na * L.cs / 4;  // cs is a multiple of 4
-  for (int i = lane; i < n4; i += 64) ((float4*)lg)[i] = ((const float4*)src)[i];
-  __syncthreads();
-  if (lane >= na) return;
-  const int r = r0 + lane;
-  const int a = h.start[l] + r;
-  const int y = r / L.W, x = r - (r / L.W) * L.W;
-  const float* px = lg + lane * L.cs;
-  float d[4];
+  const int tid = threadIdx.x;
+  const int cs4 = L.cs / 4, ls4 = cs4 + 1;  // row length / LDS row stride in float4
+  const float4* src = (const float4*)(L.logits + ((size_t)b * HW + r0) * L.cs);
+  // 8 loads in flight per thread before any LDS store (a plain copy loop
+  // would wait out one HBM latency per element)
+  for (int i0 = tid; i0 < na * cs4; i0 += 8 * 256) {
+    float4 v[8];
 #pragma unroll
-  for (int sd = 0; sd < 4; ++sd) {
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 256;
+      if (i < na * cs4) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 256;
+      if (i < na * cs4) {
+        const int row = i / cs4, c4 = i - (i / cs4) * cs4;
+        ((float4*)lg)[row * ls4 + c4] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  const int an = tid >> 2, part = tid & 3;
+  const bool live = an < na;
+  const float* px = lg + (live ? an : 0) * (L.cs + 4);
+  // DFL side `part`
+  float d;
+  {
     float v[REG];
     float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < REG; ++i) {
-      v[i] = px[sd * REG + i];
+      v[i] = px[part * REG + i];
       mx = fmaxf(mx, v[i]);
     }
     float sum = 0.f;
@@ -791,31 +1062,58 @@ __global__ __launch_bounds__(64) void detect_decode_kernel(HeadLevels h, int B, 
     float e = 0.f;
 #pragma unroll
     for (int i = 0; i < REG; ++i) e += (float)i * (v[i] / sum);
-    d[sd] = e;
+    d = e;
   }
-  const float ax = (float)x + 0.5f, ay = (float)y + 0.5f;
-  const float x1 = ax - d[0], y1 = ay - d[1], x2 = ax + d[2], y2 = ay + d[3];
-  const float cx = (x1 + x2) / 2.0f * L.stride, cy = (y1 + y2) / 2.0f * L.stride;
-  const float w = (x2 - x1) * L.stride, hh = (y2 - y1) * L.stride;
+  // classes part, part+4, ...: first maximum of the sigmoid scores
+  const float* pc = px + 4 * REG;
   float best = -1.f;
   int bc = 0;
-  const float* pc = px + 4 * REG;
-  for (int c = 0; c < nc; ++c) {
+  for (int c = part; c < nc; c += 4) {
     const float sg = 1.0f / (1.0f + __expf(-pc[c]));
-    if (raw) raw[((size_t)b * (4 + nc) + 4 + c) * A + a] = sg;
     if (sg > best) {
       best = sg;
       bc = c;
     }
   }
-  if (raw) {
-    raw[((size_t)b * (4 + nc) + 0) * A + a] = cx;
-    raw[((size_t)b * (4 + nc) + 1) * A + a] = cy;
-    raw[((size_t)b * (4 + nc) + 2) * A + a] = w;
-    raw[((size_t)b * (4 + nc) + 3) * A + a] = hh;
+  // quad reduction: larger score, then smaller class index
+#pragma unroll
+  for (int off = 1; off < 4; off <<= 1) {
+    const float ob = __shfl_xor(best, off);
+    const int oc = __shfl_xor(bc, off);
+    if (ob > best || (ob == best && oc < bc)) {
+      best = ob;
+      bc = oc;
+    }
   }
-  if (cand && best > conf) {
-    const int i = atomicAdd(&cand_n[b], 1);
+  const int base = tid & ~3;
+  const float d0 = __shfl(d, base), d1 = __shfl(d, base + 1), d2 = __shfl(d, base + 2),
+              d3 = __shfl(d, base + 3);
+  const int r = r0 + (live ? an : 0);
+  const int a = h.start[l] + r;
+  const int y = r / L.W, x = r - (r / L.W) * L.W;
+  const float ax = (float)x + 0.5f, ay = (float)y + 0.5f;
+  const float x1 = ax - d0, y1 = ay - d1, x2 = ax + d2, y2 = ay + d3;
+  const float cx = (x1 + x2) / 2.0f * L.stride, cy = (y1 + y2) / 2.0f * L.stride;
+  const float w = (x2 - x1) * L.stride, hh = (y2 - y1) * L.stride;
+  if (raw && live) {
+    for (int c = part; c < nc; c += 4)
+      raw[((size_t)b * (4 + nc) + 4 + c) * A + a] = 1.0f / (1.0f + __expf(-pc[c]));
+    const float bx[4] = {cx, cy, w, hh};
+    raw[((size_t)b * (4 + nc) + part) * A + a] = bx[part];
+  }
+  // one atomic per wave: ballot the passing anchors, the first of them
+  // reserves the wave's slots, lanes take their prefix rank
+  const bool pass = live && part == 0 && cand && best > conf;
+  const unsigned long long m = __ballot(pass);
+  if (m == 0ull) return;
+  const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  const int lead = __ffsll((long long)m) - 1;
+  int base0 = 0;
+  if ((tid & 63) == lead) base0 = atomicAdd(&cand_n[b], __popcll(m));
+  base0 = __shfl(base0, lead);
+  if (pass) {
+    const int i = base0 + rank;
     if (i < cap) {
       const float hw = w / 2.0f, hh2 = hh / 2.0f;  // xywh2xyxy
       Cand c;
@@ -852,7 +1150,7 @@ int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_ma
       return RV_EINVAL;
     }
   }
-  const size_t smem = (size_t)64 * cs * 4;
+  const size_t smem = (size_t)64 * (cs + 4) * 4;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)detect_decode_kernel<16>,
@@ -860,8 +1158,8 @@ int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_ma
     (void)hipGetLastError();
     attr = true;
   }
-  detect_decode_kernel<16><<<dim3(h.blk[nlv], B), 64, smem, s>>>(h, B, nc, conf, raw, cand,
-                                                                 cand_cap, cand_n);
+  detect_decode_kernel<16><<<dim3(h.blk[nlv], B), 256, smem, s>>>(h, B, nc, conf, raw, cand,
+                                                                  cand_cap, cand_n);
   return launch_status("detect_decode");
 }
 

@@ -10,20 +10,9 @@
 // At 1920x1080 the scale is exactly 1/3, every source coordinate is integral
 // (3x+1, 3y+1) and the resize is an exact decimation; at 640x640 and 640x480
 // it is the identity.
-#include <math.h>
-#include "common.h"
+#include "lbgeo.h"
 
 namespace rv {
-
-struct LbGeo {
-  int out_h, out_w, new_h, new_w, top, left;
-  double scale_x, scale_y;  // source / destination
-};
-
-__device__ __forceinline__ int round_short(float v) {
-  int r = __float2int_rn(v);
-  return r < -32768 ? -32768 : (r > 32767 ? 32767 : r);
-}
 
 // One thread per output pixel.
 __global__ __launch_bounds__(256) void letterbox_kernel(const uint8_t* __restrict__ in,
@@ -49,42 +38,55 @@ __global__ __launch_bounds__(256) void letterbox_kernel(const uint8_t* __restric
     dst[2] = s[2];
     return;
   }
-  // horizontal coefficients (resizeGeneric_ xofs/ialpha)
-  float fx = (float)((dx + 0.5) * g.scale_x - 0.5);
-  int sx = (int)floorf(fx);
-  fx -= (float)sx;
-  if (sx < 0) {
-    fx = 0.f;
-    sx = 0;
-  }
-  bool single = false;
-  if (sx >= W - 1) {
-    fx = 0.f;
-    sx = W - 1;
-    single = true;
-  }
-  const int a0 = round_short((1.f - fx) * 2048.f), a1 = round_short(fx * 2048.f);
-  // vertical coefficients (yofs/ibeta); rows clamped, weights kept
-  float fy = (float)((dy + 0.5) * g.scale_y - 0.5);
-  int sy = (int)floorf(fy);
-  fy -= (float)sy;
-  const int b0 = round_short((1.f - fy) * 2048.f), b1 = round_short(fy * 2048.f);
-  const int r0 = min(max(sy, 0), H - 1), r1 = min(max(sy + 1, 0), H - 1);
-  const uint8_t* s0 = frame + (size_t)r0 * pitch + (size_t)sx * 3;
-  const uint8_t* s1 = frame + (size_t)r1 * pitch + (size_t)sx * 3;
+  const LbTap tx = lb_tap_x(dx, g.scale_x, W), ty = lb_tap_y(dy, g.scale_y, H);
+  const uint8_t* r0 = frame + (size_t)ty.s0 * pitch;
+  const uint8_t* r1 = frame + (size_t)ty.s1 * pitch;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    int d0, d1;
-    if (single) {
-      d0 = s0[c] * 2048;
-      d1 = s1[c] * 2048;
-    } else {
-      d0 = s0[c] * a0 + s0[c + 3] * a1;
-      d1 = s1[c] * a0 + s1[c + 3] * a1;
-    }
-    // VResizeLinear<uchar, int, short, FixedPtCast<int,uchar,22>>
-    dst[c] = (uint8_t)((((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2);
+    const int d0 = r0[tx.s0 * 3 + c] * tx.w0 + r0[tx.s1 * 3 + c] * tx.w1;
+    const int d1 = r1[tx.s0 * 3 + c] * tx.w0 + r1[tx.s1 * 3 + c] * tx.w1;
+    dst[c] = (uint8_t)lb_vmix(d0, d1, ty.w0, ty.w1);
   }
+}
+
+// The constant-114 border of a letterbox whose interior another kernel
+// writes (the fused preprocess pass): only the pad pixels are touched.
+__global__ __launch_bounds__(256) void letterbox_pad_kernel(uint8_t* __restrict__ out, LbGeo g) {
+  const int b = blockIdx.y;
+  const int right = g.out_w - g.left - g.new_w;
+  const int band = g.top * g.out_w;                             // top rows
+  const int bottom = (g.out_h - g.top - g.new_h) * g.out_w;     // bottom rows
+  const int side = g.new_h * (g.left + right);                  // left/right columns
+  const int n = band + bottom + side;
+  uint8_t* img = out + (size_t)b * g.out_h * g.out_w * 3;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    int oy, ox;
+    if (i < band) {
+      oy = i / g.out_w;
+      ox = i - oy * g.out_w;
+    } else if (i < band + bottom) {
+      const int j = i - band;
+      oy = g.top + g.new_h + j / g.out_w;
+      ox = j - (j / g.out_w) * g.out_w;
+    } else {
+      const int j = i - band - bottom;
+      const int w = g.left + right;
+      oy = g.top + j / w;
+      const int c = j - (j / w) * w;
+      ox = c < g.left ? c : g.left + g.new_w + (c - g.left);
+    }
+    uint8_t* d = img + ((size_t)oy * g.out_w + ox) * 3;
+    d[0] = 114;
+    d[1] = 114;
+    d[2] = 114;
+  }
+}
+
+int launch_letterbox_pad(uint8_t* out, int B, const LbGeo& g, hipStream_t s) {
+  const int n = g.out_h * g.out_w - g.new_h * g.new_w;
+  if (n <= 0 || B == 0) return RV_OK;
+  letterbox_pad_kernel<<<dim3(ceil_div(n, 256), B), 256, 0, s>>>(out, g);
+  return launch_status("letterbox_pad");
 }
 
 }  // namespace rv
@@ -116,19 +118,8 @@ extern "C" int rv_letterbox_u8(const uint8_t* in, uint8_t* out, int B, int H, in
   RV_CHECK_ARG(in != nullptr && out != nullptr && geo != nullptr, "null pointer");
   RV_CHECK_ARG(B >= 0 && H > 0 && W > 0 && pitch >= 3 * W, "bad frame shape");
   LbGeo g;
-  g.out_h = geo[0];
-  g.out_w = geo[1];
-  g.new_h = geo[2];
-  g.new_w = geo[3];
-  g.top = geo[4];
-  g.left = geo[5];
-  RV_CHECK_ARG(g.new_h > 0 && g.new_w > 0 && g.top >= 0 && g.left >= 0 &&
-                   g.top + g.new_h <= g.out_h && g.left + g.new_w <= g.out_w,
-               "inconsistent letterbox geometry");
+  RV_CHECK_ARG(lbgeo_from(geo, H, W, g), "inconsistent letterbox geometry");
   if (B == 0) return RV_OK;
-  // cv::resize: inv_scale = dsize/ssize, scale = 1/inv_scale
-  g.scale_x = 1.0 / ((double)g.new_w / W);
-  g.scale_y = 1.0 / ((double)g.new_h / H);
   dim3 grid(ceil_div(g.out_w, 256), g.out_h, B);
   letterbox_kernel<<<grid, 256, 0, as_stream(stream)>>>(in, out, H, W, pitch, g);
   return launch_status("rv_letterbox_u8");

@@ -13,7 +13,7 @@
 //
 // HBM layout: frames are B x H x pitch bytes (interleaved BGR).  The LUT
 // workspace is B x tiles^2 x 256 u8 (16 KB per frame at 8x8).
-#include "common.h"
+#include "lbgeo.h"
 
 namespace rv {
 
@@ -79,21 +79,33 @@ __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restric
   if (vec) {
     const int groups = g.tw >> 2;
     const int total = groups * g.th;
-    for (int i = t; i < total; i += 256) {
-      const int r = i / groups;
-      const int gi = i - r * groups;
-      const uint32_t* p =
-          (const uint32_t*)(frame + (size_t)(y0 + r) * pitch + (size_t)(x0 + gi * 4) * 3);
-      const uint32_t w0 = p[0], w1 = p[1], w2 = p[2];
-      // bytes little-endian: w0 = b0 g0 r0 b1 | w1 = g1 r1 b2 g2 | w2 = r2 b3 g3 r3
-      const int y_0 = bgr_to_y(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255);
-      const int y_1 = bgr_to_y(w0 >> 24, w1 & 255, (w1 >> 8) & 255);
-      const int y_2 = bgr_to_y((w1 >> 16) & 255, w1 >> 24, w2 & 255);
-      const int y_3 = bgr_to_y((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24);
-      atomicAdd(&h[y_0], 1);
-      atomicAdd(&h[y_1], 1);
-      atomicAdd(&h[y_2], 1);
-      atomicAdd(&h[y_3], 1);
+    // 4 groups in flight per thread (the loop is load-latency bound)
+    for (int i0 = t; i0 < total; i0 += 4 * 256) {
+      uint32_t w[4][3];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 256;
+        w[u][0] = w[u][1] = w[u][2] = 0;
+        if (i < total) {
+          const int r = i / groups;
+          const int gi = i - r * groups;
+          const uint32_t* p =
+              (const uint32_t*)(frame + (size_t)(y0 + r) * pitch + (size_t)(x0 + gi * 4) * 3);
+          w[u][0] = p[0];
+          w[u][1] = p[1];
+          w[u][2] = p[2];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (i0 + u * 256 >= total) break;
+        const uint32_t w0 = w[u][0], w1 = w[u][1], w2 = w[u][2];
+        // bytes little-endian: w0 = b0 g0 r0 b1 | w1 = g1 r1 b2 g2 | w2 = r2 b3 g3 r3
+        atomicAdd(&h[bgr_to_y(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255)], 1);
+        atomicAdd(&h[bgr_to_y(w0 >> 24, w1 & 255, (w1 >> 8) & 255)], 1);
+        atomicAdd(&h[bgr_to_y((w1 >> 16) & 255, w1 >> 24, w2 & 255)], 1);
+        atomicAdd(&h[bgr_to_y((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24)], 1);
+      }
     }
   } else {
     const int total = g.tw * g.th;
@@ -402,6 +414,326 @@ __global__ __launch_bounds__(256) void median_tile_kernel(const uint8_t* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// 3x3 fast path: med3_kernel<CLAHE, LB>.
+// Block = 256 threads -> 128 x 32 output pixels of one frame.
+//  1. (CLAHE) the block's interpolation cells go to LDS as packed u32
+//     entries: cell (cy, cx) = the 4 tile LUTs one pixel blends, so a pixel
+//     costs ONE ds_read_b32 for its l11|l12|l21|l22.
+//  2. the (32+2) x (128+8) halo tile is loaded in 4-pixel groups (12 bytes,
+//     three dword loads, all issued before any use), CLAHE'd in registers
+//     and stored to LDS as 3 dwords per group.
+//  3. each thread produces a 4 x 4 block of medians (4 px wide, 4 rows):
+//     it reads 6 tile rows x 20 bytes with dword loads, sorts every 3-row
+//     column once (min3/med3/max3) and combines 3 columns per output:
+//     med = med3(max3(lo), med3(mid), min3(hi))  -- exact for 9 samples.
+//  4. (LB) medians are also kept in LDS and the letterbox pixels whose
+//     bilinear support lies in this block are produced from them
+//     (cv2.resize INTER_LINEAR fixed point, lbgeo.h).  The host only picks
+//     LB when every letterbox pixel's support falls inside one block.
+// ---------------------------------------------------------------------------
+constexpr int kM3W = 128, kM3H = 32;
+constexpr int kM3TW = kM3W + 8;         // tile px x0-4 .. x0+131
+constexpr int kM3TH = kM3H + 2;         // tile rows y0-1 .. y0+32
+constexpr int kM3Groups = kM3TW / 4;    // 34 four-pixel groups per row
+constexpr int kM3Stride = 416;          // tile row bytes (408 used)
+constexpr int kM3OStride = kM3W * 3 + 16;  // median tile row bytes (LB)
+constexpr int kCellMax = 16;            // packed LUT cells per block (16 KB)
+constexpr int kM3Iter = (kM3TH * kM3Groups + 255) / 256;  // 5
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// v_med3_u32 (written out: the min/max form gets CSE'd with the column
+// min3/max3 and loses the 3-input instructions)
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+struct LbFuse {
+  LbGeo g;
+  uint8_t* out;  // B x out_h x out_w x 3
+};
+
+__device__ __forceinline__ int clahe_cell_index(int p, float inv) {
+  return (int)floorf((float)p * inv - 0.5f);
+}
+
+template <bool CLAHE, bool LB>
+__global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ in,
+                                                   uint8_t* __restrict__ out,
+                                                   const uint8_t* __restrict__ lut, int H, int W,
+                                                   int pitch, int vec, ClaheGeo g, LbFuse lb) {
+  constexpr int kUnion = CLAHE ? (LB ? (kCellMax * 1024 > kM3H * kM3OStride ? kCellMax * 1024
+                                                                             : kM3H * kM3OStride)
+                                     : kCellMax * 1024)
+                               : (LB ? kM3H * kM3OStride : 16);
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kM3TH * kM3Stride];
+  __shared__ __attribute__((aligned(16))) uint8_t uni[kUnion];  // cells, then the median tile
+  uint32_t* cells = (uint32_t*)uni;
+
+  const int tid = threadIdx.x;
+  const int b = blockIdx.z;
+  const int x0 = blockIdx.x * kM3W, y0 = blockIdx.y * kM3H;
+  const uint8_t* frame = in + (size_t)b * H * pitch;
+
+  // ---- 1. packed LUT cells of this block
+  int cx0 = 0, cy0 = 0, ncx = 1;
+  if constexpr (CLAHE) {
+    const int gx_lo = max(x0 - 4, 0), gx_hi = min(x0 + kM3TW - 5, W - 1);
+    const int gy_lo = max(y0 - 1, 0), gy_hi = min(y0 + kM3H, H - 1);
+    cx0 = clahe_cell_index(gx_lo, g.inv_tw);
+    cy0 = clahe_cell_index(gy_lo, g.inv_th);
+    ncx = clahe_cell_index(gx_hi, g.inv_tw) - cx0 + 1;
+    const int ncy = clahe_cell_index(gy_hi, g.inv_th) - cy0 + 1;
+    const uint8_t* flut = lut + (size_t)b * g.tiles * g.tiles * 256;
+    const int Y = tid;  // one LUT entry per thread per cell
+    for (int c = 0; c < ncx * ncy; ++c) {
+      const int cy = c / ncx, cx = c - (c / ncx) * ncx;
+      const int iy = cy0 + cy, ix = cx0 + cx;
+      const int r1 = max(iy, 0), r2 = min(iy + 1, g.tiles - 1);
+      const int c1 = max(ix, 0), c2 = min(ix + 1, g.tiles - 1);
+      const uint32_t l11 = flut[(r1 * g.tiles + c1) * 256 + Y];
+      const uint32_t l12 = flut[(r1 * g.tiles + c2) * 256 + Y];
+      const uint32_t l21 = flut[(r2 * g.tiles + c1) * 256 + Y];
+      const uint32_t l22 = flut[(r2 * g.tiles + c2) * 256 + Y];
+      cells[c * 256 + Y] = l11 | (l12 << 8) | (l21 << 16) | (l22 << 24);
+    }
+  }
+
+  // ---- 2. halo tile: thread -> one 4-pixel column group (gc) and the rows
+  //      r0, r0+7, ... (so the per-pixel x interpolation is computed once);
+  //      every load is issued before any use.
+  constexpr int kRowStep = 256 / kM3Groups;  // 7 (238 threads busy)
+  constexpr int kIt = (kM3TH + kRowStep - 1) / kRowStep;  // 5
+  const int gc = tid % kM3Groups, r0 = tid / kM3Groups;
+  const bool s2 = r0 < kRowStep;
+  const int px0 = x0 - 4 + gc * 4;
+  const bool vrow = vec && px0 >= 0 && px0 + 3 < W;
+  uint32_t d[kIt][3];
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int hr = r0 + it * kRowStep;
+    d[it][0] = d[it][1] = d[it][2] = 0;
+    if (s2 && hr < kM3TH) {
+      const int gy = min(max(y0 - 1 + hr, 0), H - 1);
+      const uint8_t* row = frame + (size_t)gy * pitch;
+      if (vrow) {
+        const uint32_t* p = (const uint32_t*)(row + px0 * 3);
+        d[it][0] = p[0];
+        d[it][1] = p[1];
+        d[it][2] = p[2];
+      } else {
+        uint8_t v[12];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int gx = min(max(px0 + j, 0), W - 1);
+          v[3 * j] = row[gx * 3];
+          v[3 * j + 1] = row[gx * 3 + 1];
+          v[3 * j + 2] = row[gx * 3 + 2];
+        }
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+          d[it][w] = v[4 * w] | (v[4 * w + 1] << 8) | (v[4 * w + 2] << 16) |
+                     ((uint32_t)v[4 * w + 3] << 24);
+      }
+    }
+  }
+  // per-pixel x interpolation (CLAHE_Interpolation_Body xa/xa1/ind)
+  f32x2 xw[4];   // {xa1, xa}
+  int xoff[4];   // cell column offset * 256
+  if constexpr (CLAHE) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int gx = min(max(px0 + j, 0), W - 1);
+      const float fx = (float)gx * g.inv_tw - 0.5f;
+      const int ix = (int)floorf(fx);
+      const float xa = fx - (float)ix;
+      xw[j] = f32x2{1.0f - xa, xa};
+      xoff[j] = (ix - cx0) * 256;
+    }
+    __syncthreads();  // cells visible
+  }
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int hr = r0 + it * kRowStep;
+    if (!s2 || hr >= kM3TH) break;
+    uint32_t* dst = (uint32_t*)(tile + hr * kM3Stride + gc * 12);
+    if constexpr (CLAHE) {
+      const int gy = min(max(y0 - 1 + hr, 0), H - 1);
+      const float fy = (float)gy * g.inv_th - 0.5f;
+      const int iy = (int)floorf(fy);
+      const float ya = fy - (float)iy;
+      const f32x2 yw = {1.0f - ya, ya};
+      const uint32_t* crow = cells + (iy - cy0) * ncx * 256;
+      uint32_t o[3] = {0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int bb = (d[it][(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255;
+        const int gg = (d[it][(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255;
+        const int rr = (d[it][(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255;
+        int Y, Cr, Cb;
+        bgr_to_ycrcb(bb, gg, rr, Y, Cr, Cb);
+        const uint32_t q = crow[xoff[j] + Y];
+        // (l11*xa1 + l12*xa, l21*xa1 + l22*xa) as one packed-f32 pair, then
+        // top*ya1 + bottom*ya: the scalar expression's exact op order
+        const f32x2 l1 = {(float)(q & 255), (float)((q >> 16) & 255)};
+        const f32x2 l2 = {(float)((q >> 8) & 255), (float)(q >> 24)};
+        const f32x2 tb = l1 * xw[j].x + l2 * xw[j].y;
+        const f32x2 tw = tb * yw;
+        const int y2 = sat_u8(__float2int_rn(tw.x + tw.y));
+        int ob, og, orr;
+        ycrcb_to_bgr(y2, Cr, Cb, ob, og, orr);
+        o[(3 * j) >> 2] |= (uint32_t)ob << (8 * ((3 * j) & 3));
+        o[(3 * j + 1) >> 2] |= (uint32_t)og << (8 * ((3 * j + 1) & 3));
+        o[(3 * j + 2) >> 2] |= (uint32_t)orr << (8 * ((3 * j + 2) & 3));
+      }
+      dst[0] = o[0];
+      dst[1] = o[1];
+      dst[2] = o[2];
+    } else {
+      dst[0] = d[it][0];
+      dst[1] = d[it][1];
+      dst[2] = d[it][2];
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. medians: thread -> 4 px (rx..rx+3) x 4 rows (ry..ry+3)
+  const int rx = (tid & 31) * 4, ry = (tid >> 5) * 4;
+  uint32_t rw[6][5];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const uint32_t* p = (const uint32_t*)(tile + (ry + r) * kM3Stride + rx * 3 + 8);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) rw[r][j] = p[j];
+  }
+  // byte (column jj in 0..5 = px rx-1+jj, channel c) of row r sits at window
+  // byte 1 + 3*jj + c
+#define RV_B(r, k) ((rw[r][(k) >> 2] >> (8 * ((k) & 3))) & 255u)
+  uint8_t* fout = out + (size_t)b * H * pitch;
+  const int x = x0 + rx;
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    const int y = y0 + ry + o;
+    uint32_t res[3] = {0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      uint32_t lo[6], mi[6], hi[6];
+#pragma unroll
+      for (int jj = 0; jj < 6; ++jj) {
+        const uint32_t a = RV_B(o, 1 + 3 * jj + c), bq = RV_B(o + 1, 1 + 3 * jj + c),
+                       e = RV_B(o + 2, 1 + 3 * jj + c);
+        lo[jj] = min(min(a, bq), e);
+        hi[jj] = max(max(a, bq), e);
+        mi[jj] = med3_u32(a, bq, e);
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const uint32_t l = max(max(lo[p], lo[p + 1]), lo[p + 2]);
+        const uint32_t m = med3_u32(mi[p], mi[p + 1], mi[p + 2]);
+        const uint32_t h = min(min(hi[p], hi[p + 1]), hi[p + 2]);
+        const uint32_t v = med3_u32(l, m, h);
+        const int k = 3 * p + c;
+        res[k >> 2] |= v << (8 * (k & 3));
+      }
+    }
+    if constexpr (LB) {
+      uint32_t* od = (uint32_t*)(uni + (ry + o) * kM3OStride + rx * 3);
+      od[0] = res[0];
+      od[1] = res[1];
+      od[2] = res[2];
+    }
+    if (y < H && x < W) {
+      uint8_t* dst = fout + (size_t)y * pitch + (size_t)x * 3;
+      if (vec && x + 3 < W) {
+        ((uint32_t*)dst)[0] = res[0];
+        ((uint32_t*)dst)[1] = res[1];
+        ((uint32_t*)dst)[2] = res[2];
+      } else {
+        const int n = min(4, W - x) * 3;
+        for (int j = 0; j < n; ++j) dst[j] = (uint8_t)(res[j >> 2] >> (8 * (j & 3)));
+      }
+    }
+  }
+#undef RV_B
+
+  // ---- 4. letterbox pixels owned by this block: per-axis taps once into
+  //      LDS (after the cells region, which is free again), then 2-D
+  if constexpr (LB) {
+    __shared__ LbTap tapx[kM3W + 8], tapy[kM3H + 8];
+    __shared__ int ntap[2], dlo[2];
+    const LbGeo& G = lb.g;
+    if (tid < 2) {
+      const double inv = tid == 0 ? 1.0 / G.scale_x : 1.0 / G.scale_y;
+      const int o0 = tid == 0 ? x0 : y0, span = tid == 0 ? kM3W : kM3H;
+      const int nmax = tid == 0 ? G.new_w : G.new_h;
+      const int lo = max(0, (int)floor((o0 + 0.5) * inv - 0.5) - 2);
+      const int hi = min(nmax - 1, (int)ceil((o0 + span - 0.5) * inv - 0.5) + 2);
+      dlo[tid] = lo;
+      ntap[tid] = max(0, min(hi - lo + 1, span + 8));
+    }
+    __syncthreads();  // also: the median tile is complete
+    const int nx = ntap[0], ny = ntap[1];
+    if (tid < nx) tapx[tid] = lb_tap_x(dlo[0] + tid, G.scale_x, W);
+    else if (tid >= 192 && tid - 192 < ny) tapy[tid - 192] = lb_tap_y(dlo[1] + tid - 192, G.scale_y, H);
+    __syncthreads();
+    uint8_t* lbo = lb.out + (size_t)b * G.out_h * G.out_w * 3;
+    for (int i = tid; i < nx * ny; i += 256) {
+      const int jy = i / nx, jx = i - (i / nx) * nx;
+      const LbTap tx = tapx[jx], ty = tapy[jy];
+      // owner: the block holding the first tap (host checked: all taps)
+      if (tx.s0 < x0 || tx.s0 >= x0 + kM3W || ty.s0 < y0 || ty.s0 >= y0 + kM3H) continue;
+      const uint8_t* r0 = uni + (ty.s0 - y0) * kM3OStride;
+      const uint8_t* r1 = uni + (ty.s1 - y0) * kM3OStride;
+      const int c0 = (tx.s0 - x0) * 3, c1 = (tx.s1 - x0) * 3;
+      uint8_t* dst = lbo + ((size_t)(G.top + dlo[1] + jy) * G.out_w + G.left + dlo[0] + jx) * 3;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int d0 = r0[c0 + c] * tx.w0 + r0[c1 + c] * tx.w1;
+        const int d1 = r1[c0 + c] * tx.w0 + r1[c1 + c] * tx.w1;
+        dst[c] = (uint8_t)lb_vmix(d0, d1, ty.w0, ty.w1);
+      }
+    }
+  }
+}
+
+// Host checks for med3_kernel.
+static bool med3_cells_fit(const ClaheGeo& g, int H, int W) {
+  // distinct floor(p/t - 0.5) over a span of n consecutive p <= ceil(n/t) + 1
+  // (+1 more for float rounding of p * inv)
+  const int ncx = min((kM3TW + g.tw - 1) / g.tw + 2, g.tiles + 1);
+  const int ncy = min((kM3TH + g.th - 1) / g.th + 2, g.tiles + 1);
+  (void)H;
+  (void)W;
+  return ncx * ncy <= kCellMax;
+}
+
+// every letterbox pixel's nonzero taps must lie in the block of its first tap
+static bool med3_lb_fits(const LbGeo& G, int H, int W) {
+  // downscale / identity only: a block then owns <= 128 + 5 columns and
+  // <= 32 + 5 rows of letterbox pixels (the LDS tap tables)
+  if (G.new_w > W || G.new_h > H) return false;
+  for (int dx = 0; dx < G.new_w; ++dx) {
+    const LbTap t = lb_tap_x(dx, G.scale_x, W);
+    if (t.s0 / kM3W != t.s1 / kM3W) return false;
+  }
+  for (int dy = 0; dy < G.new_h; ++dy) {
+    const LbTap t = lb_tap_y(dy, G.scale_y, H);
+    if (t.s0 / kM3H != t.s1 / kM3H) return false;
+  }
+  return true;
+}
+
+template <bool CLAHE, bool LB>
+static void launch_med3(const uint8_t* in, uint8_t* out, const uint8_t* lut, int B, int H, int W,
+                        int pitch, const ClaheGeo& g, const LbFuse& lb, hipStream_t s) {
+  const int vec = (pitch % 4 == 0) && (((uintptr_t)in) % 4 == 0) && (((uintptr_t)out) % 4 == 0);
+  dim3 grid(ceil_div(W, kM3W), ceil_div(H, kM3H), B);
+  med3_kernel<CLAHE, LB><<<grid, 256, 0, s>>>(in, out, lut, H, W, pitch, vec, g, lb);
+}
+
 // Gray span for the low-contrast gate (pipeline.py:24-30).
 __global__ __launch_bounds__(256) void gray_span_kernel(const uint8_t* __restrict__ in, int H,
                                                         int W, int pitch, int* __restrict__ mn_mx) {
@@ -503,7 +835,10 @@ extern "C" int rv_median_u8c3(const uint8_t* in, uint8_t* out, int B, int H, int
   RV_CHECK_ARG(k == 3 || k == 5 || k == 7 || k == 9, "median k=%d must be 3,5,7,9", k);
   if (B == 0) return RV_OK;
   ClaheGeo g{};
-  dispatch_median<false>(k, in, out, nullptr, B, H, W, pitch, g, as_stream(stream));
+  if (k == 3)
+    launch_med3<false, false>(in, out, nullptr, B, H, W, pitch, g, LbFuse{}, as_stream(stream));
+  else
+    dispatch_median<false>(k, in, out, nullptr, B, H, W, pitch, g, as_stream(stream));
   return launch_status("rv_median_u8c3");
 }
 
@@ -519,6 +854,11 @@ extern "C" int rv_clahe_median_u8(const uint8_t* in, uint8_t* out, int B, int H,
   ClaheGeo g = make_geo(H, W, tiles, clip);
   hipStream_t s = as_stream(stream);
   uint8_t* lut = (uint8_t*)ws;
+  if (k == 3 && med3_cells_fit(g, H, W)) {
+    clahe_lut_kernel<<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+    launch_med3<true, false>(in, out, lut, B, H, W, pitch, g, LbFuse{}, s);
+    return launch_status("rv_clahe_median_u8");
+  }
   RV_CHECK_ARG(lut_window_fits(g, k),
                "LUT window too large for the fused pass (tiles=%d, tile %dx%d); "
                "use rv_clahe_ycrcb_u8 + rv_median_u8c3",
@@ -530,7 +870,42 @@ extern "C" int rv_clahe_median_u8(const uint8_t* in, uint8_t* out, int B, int H,
 
 extern "C" int rv_clahe_median_fits(int H, int W, int tiles, int k) {
   if (H <= 0 || W <= 0 || tiles < 1 || tiles > 64) return 0;
-  return lut_window_fits(make_geo(H, W, tiles, 0.0), k) ? 1 : 0;
+  const ClaheGeo g = make_geo(H, W, tiles, 0.0);
+  if (k == 3 && med3_cells_fit(g, H, W)) return 1;
+  return lut_window_fits(g, k) ? 1 : 0;
+}
+
+extern "C" int rv_clahe_median_letterbox_fits(int H, int W, int tiles, int k, const int* geo) {
+  if (H <= 0 || W <= 0 || tiles < 1 || tiles > 64 || k != 3 || geo == nullptr) return 0;
+  LbGeo G;
+  if (!lbgeo_from(geo, H, W, G)) return 0;
+  return med3_cells_fit(make_geo(H, W, tiles, 0.0), H, W) && med3_lb_fits(G, H, W) ? 1 : 0;
+}
+
+extern "C" int rv_clahe_median_letterbox_u8(const uint8_t* in, uint8_t* out, int B, int H, int W,
+                                            int pitch, int tiles, double clip, int k, void* ws,
+                                            size_t ws_bytes, uint8_t* lb_out, const int* geo,
+                                            void* stream) {
+  int st = check_frames(in, out, B, H, W, pitch);
+  if (st) return st;
+  RV_CHECK_ARG(tiles >= 1 && tiles <= 64, "tiles %d out of range", tiles);
+  RV_CHECK_ARG(ws != nullptr && ws_bytes >= rv_clahe_ws_bytes(B, tiles), "workspace too small");
+  RV_CHECK_ARG(lb_out != nullptr && geo != nullptr, "null letterbox pointer");
+  RV_CHECK_ARG(rv_clahe_median_letterbox_fits(H, W, tiles, k, geo),
+               "geometry not supported by the fused pass (k=%d, %dx%d, tiles=%d); use "
+               "rv_clahe_median_u8 + rv_letterbox_u8", k, W, H, tiles);
+  if (B == 0) return RV_OK;
+  ClaheGeo g = make_geo(H, W, tiles, clip);
+  LbFuse lb;
+  lbgeo_from(geo, H, W, lb.g);
+  lb.out = lb_out;
+  hipStream_t s = as_stream(stream);
+  uint8_t* lut = (uint8_t*)ws;
+  st = launch_letterbox_pad(lb_out, B, lb.g, s);
+  if (st) return st;
+  clahe_lut_kernel<<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  launch_med3<true, true>(in, out, lut, B, H, W, pitch, g, lb, s);
+  return launch_status("rv_clahe_median_letterbox_u8");
 }
 
 extern "C" int rv_gray_span_u8(const uint8_t* in, int B, int H, int W, int pitch, int* ws,

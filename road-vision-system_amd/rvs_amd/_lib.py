@@ -33,6 +33,10 @@ _SIGS = {
     "rv_clahe_median_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                    c_double, c_int, c_void_p, c_size_t, c_void_p]),
     "rv_clahe_median_fits": (c_int, [c_int, c_int, c_int, c_int]),
+    "rv_clahe_median_letterbox_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                             c_int, c_double, c_int, c_void_p, c_size_t,
+                                             c_void_p, POINTER(c_int), c_void_p]),
+    "rv_clahe_median_letterbox_fits": (c_int, [c_int, c_int, c_int, c_int, POINTER(c_int)]),
     "rv_gray_span_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                 c_void_p]),
     "rv_letterbox_geometry": (c_int, [c_int, c_int, c_int, c_int, POINTER(c_int)]),
@@ -104,7 +108,7 @@ def check(status: int, what: str = "") -> None:
         raise RVError(f"{what or 'rvhip'} failed with status {status}: {msg}")
 
 
-_NOCHECK = {"rv_abi_version", "rv_clahe_median_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
+_NOCHECK = {"rv_abi_version", "rv_clahe_median_fits", "rv_clahe_median_letterbox_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
             "rv_yolo_num_buffers", "rv_yolo_trace", "rv_yolo_profile_read"}
 
 

@@ -134,6 +134,11 @@ class YoloEngine:
         self.forward_raw(self.letterbox(frames))
         return self.nms(B)
 
+    def run_letterboxed(self, lb: torch.Tensor):
+        """Already letterboxed (B,in_h,in_w,3) u8 device batch -> (dets, counts)."""
+        self.forward_raw(lb)
+        return self.nms(lb.shape[0])
+
     @staticmethod
     def to_detections(dets: torch.Tensor, det_n: torch.Tensor, names=COCO80) -> List[List[Detection]]:
         d = dets.cpu().numpy()

@@ -1,8 +1,9 @@
 """Batched per-frame hot path: S camera streams x 1 frame per step.
 
 Reproduces the reference's per-frame call order (main_preview.py:94-109):
-    proc = pipeline(raw)                 -> fused CLAHE + median (HIP)
-    dets = detector.infer(proc)          -> letterbox + YOLOv8 + NMS (HIP)
+    proc = pipeline(raw)                 -> fused CLAHE + median (HIP), which
+                                            also emits the detector's letterbox
+    dets = detector.infer(proc)          -> YOLOv8 + NMS (HIP)
     dets = tracker.update(dets, ts, projector)   -> SORT + geometry (HIP)
 for a stream-major batch, entirely on the device: no host round trip inside a
 step.  ``results()`` converts one step's device outputs into the reference's
@@ -56,11 +57,18 @@ class RoadVisionEngine:
         self.tracker.set_projector(projector)
         self.proc = torch.empty((self.S, self.H, self.W, 3), dtype=torch.uint8, device=self.device)
         self.names = COCO80
+        # default chain: CLAHE + median + the detector's LetterBox in one pass
+        self.fused_letterbox = self.pipeline.letterbox_fusable(self.H, self.W, self.detector.geo)
 
     def step(self, frames: torch.Tensor, ts: torch.Tensor) -> Dict[str, torch.Tensor]:
         """frames (S,H,W,3) u8 on device, ts (S,) f64 on device."""
-        proc = self.pipeline(frames)
-        dets, det_n = self.detector.run(proc)
+        if self.fused_letterbox:
+            proc, lb = self.pipeline.run_with_letterbox(frames, self.detector.geo,
+                                                        self.detector.lb[:frames.shape[0]])
+            dets, det_n = self.detector.run_letterboxed(lb)
+        else:
+            proc = self.pipeline(frames)
+            dets, det_n = self.detector.run(proc)
         tid, dist, spd = self.tracker.update(dets, det_n, ts)
         return {"proc": proc, "dets": dets, "det_n": det_n, "track_id": tid,
                 "distance_m": dist, "speed_kmh": spd}

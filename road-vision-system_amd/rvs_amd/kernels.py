@@ -76,6 +76,26 @@ def clahe_median(frames: torch.Tensor, tiles: int = 8, clip: float = 2.0, k: int
     return out if frames.dim() == 4 else out[0]
 
 
+def clahe_median_letterbox(frames: torch.Tensor, tiles: int, clip: float, k: int, geo,
+                           out: Optional[torch.Tensor] = None,
+                           lb_out: Optional[torch.Tensor] = None,
+                           ws: Optional[torch.Tensor] = None):
+    """Fused CLAHE + median + LetterBox: returns (proc, letterboxed)."""
+    x, B, H, W, pitch = _frames(frames)
+    out = _like(x, out)
+    if lb_out is None:
+        lb_out = torch.empty((B, geo[0], geo[1], 3), dtype=torch.uint8, device=x.device)
+    ws, need = _ws(B, tiles, ws, x.device)
+    call("rv_clahe_median_letterbox_u8", ptr(x), ptr(out), B, H, W, pitch, int(tiles),
+         float(clip), int(k), ptr(ws), ws.numel(), ptr(lb_out), _lib.int_array(geo), stream_ptr())
+    return (out if frames.dim() == 4 else out[0]), lb_out
+
+
+def clahe_median_letterbox_fits(H: int, W: int, tiles: int, k: int, geo) -> bool:
+    return bool(_lib.load().rv_clahe_median_letterbox_fits(H, W, int(tiles), int(k),
+                                                           _lib.int_array(geo)))
+
+
 def clahe_median_fits(frames: torch.Tensor, tiles: int, k: int) -> bool:
     H, W = frames.shape[-3], frames.shape[-2]
     return bool(_lib.load().rv_clahe_median_fits(H, W, int(tiles), int(k)))

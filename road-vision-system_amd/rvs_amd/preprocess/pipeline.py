@@ -58,6 +58,26 @@ class PreprocessPipeline:
             out = op(out)
         return out
 
+    def letterbox_fusable(self, H: int, W: int, geo) -> bool:
+        """True when the chain is the fused default and the detector's
+        LetterBox (geo) can be emitted by the same pass (no gate: the gate
+        selects raw frames per frame after the chain)."""
+        if not (self.enabled and self._fused) or self._gate_enabled():
+            return False
+        clahe, med = self.ops
+        return kernels.clahe_median_letterbox_fits(H, W, clahe.grid, med.k, geo)
+
+    def run_with_letterbox(self, x: torch.Tensor, geo, lb_out: torch.Tensor):
+        """(B,H,W,3) device frames -> (proc, letterboxed proc) in one pass;
+        byte-identical to self(x) followed by the detector's letterbox."""
+        clahe, med = self.ops
+        B = x.shape[0]
+        need = kernels.clahe_ws_bytes(B, clahe.grid)
+        if self._ws is None or self._ws.numel() < need or self._ws.device != x.device:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=x.device)
+        return kernels.clahe_median_letterbox(x, clahe.grid, clahe.clip_limit, med.k, geo,
+                                              lb_out=lb_out, ws=self._ws)
+
     def __call__(self, image, ts: float = None):
         if not self.enabled or not self.ops:
             return image

@@ -73,3 +73,12 @@ def test_letterbox_geometry_known_values():
     assert kernels.letterbox_geometry(1080, 1920) == (384, 640, 360, 640, 12, 0)
     assert kernels.letterbox_geometry(640, 640) == (640, 640, 640, 640, 0, 0)
     assert kernels.letterbox_geometry(480, 640) == (480, 640, 480, 640, 0, 0)
+
+
+def test_fused_letterbox_fits_host_only():
+    """rv_clahe_median_letterbox_fits is a host query (no GPU needed)."""
+    from rvs_amd import kernels
+    assert kernels.clahe_median_letterbox_fits(1080, 1920, 8, 3, kernels.letterbox_geometry(1080, 1920))
+    assert kernels.clahe_median_letterbox_fits(640, 640, 8, 3, kernels.letterbox_geometry(640, 640))
+    assert not kernels.clahe_median_letterbox_fits(1080, 1920, 8, 5,
+                                                   kernels.letterbox_geometry(1080, 1920))

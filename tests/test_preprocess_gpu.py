@@ -107,3 +107,41 @@ def test_pipeline_matches_reference_semantics(cuda):
     flat = np.full((32, 32, 3), 90, np.uint8)
     flat[0, 0] = 95
     np.testing.assert_array_equal(p2(flat), cpu.median(cpu.clahe_ycrcb(flat), 5))
+
+
+def test_median_vector_path_ragged_width(cuda):
+    """Row pitch a multiple of 4 with W % 4 != 0: dword loads/stores on the
+    interior groups, byte path on the ragged right edge."""
+    import torch
+    from rvs_amd import kernels
+    H, W = 70, 130
+    img = road_frame(H, W, seed=5)
+    wide = torch.zeros((2, H, W + 2, 3), dtype=torch.uint8, device=cuda)
+    wide[:, :, :W] = _dev(img, cuda)
+    view = wide[:, :, :W]
+    out = kernels.clahe_median(view, 8, 2.0, 3)
+    ref = cpu.median(cpu.clahe_ycrcb(img, 8, 2.0), 3)
+    for b in range(2):
+        np.testing.assert_array_equal(out[b].cpu().numpy(), ref)
+    np.testing.assert_array_equal(kernels.median(view, 3)[0].cpu().numpy(), cpu.median(img, 3))
+
+
+@pytest.mark.parametrize("H,W", [(1080, 1920), (720, 1280), (640, 640), (480, 640), (2160, 3840),
+                                 (37, 91), (300, 2000), (700, 500), (1000, 1400)])
+def test_fused_letterbox_equals_chain(cuda, H, W):
+    """rv_clahe_median_letterbox_u8 == rv_clahe_median_u8 + rv_letterbox_u8
+    == oracle (CLAHE -> median -> LetterBox), byte for byte."""
+    from rvs_amd import _lib, kernels
+    img = road_frame(H, W, seed=H + 2 * W)
+    x = _dev(np.stack([img, img[::-1].copy()]), cuda)
+    geo = kernels.letterbox_geometry(H, W)
+    if not kernels.clahe_median_letterbox_fits(H, W, 8, 3, geo):
+        with pytest.raises(_lib.RVError):
+            kernels.clahe_median_letterbox(x, 8, 2.0, 3, geo)
+        pytest.skip("geometry not eligible for the fused letterbox (checked: RV_EINVAL)")
+    proc, lb = kernels.clahe_median_letterbox(x, 8, 2.0, 3, geo)
+    chain = kernels.clahe_median(x, 8, 2.0, 3)
+    np.testing.assert_array_equal(proc.cpu().numpy(), chain.cpu().numpy())
+    np.testing.assert_array_equal(lb.cpu().numpy(), kernels.letterbox(chain, geo).cpu().numpy())
+    ref = cpu.letterbox(cpu.median(cpu.clahe_ycrcb(img, 8, 2.0), 3), geo)
+    np.testing.assert_array_equal(lb[0].cpu().numpy(), ref)

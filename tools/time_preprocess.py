@@ -36,6 +36,8 @@ for name, fn, nbytes in [
     ("clahe_ycrcb", lambda: kernels.clahe_ycrcb(x, 8, 2.0, out=out, ws=ws), 3 * frame_bytes),
     ("median3", lambda: kernels.median(x, 3, out=out), 2 * frame_bytes),
     ("clahe_median", lambda: kernels.clahe_median(x, 8, 2.0, 3, out=out, ws=ws), 3 * frame_bytes),
+    ("clahe_med_lb", lambda: kernels.clahe_median_letterbox(x, 8, 2.0, 3, geo, out=out, lb_out=lb,
+                                                             ws=ws), 3 * frame_bytes),
     ("letterbox", lambda: kernels.letterbox(out, geo, out=lb), frame_bytes / 3 + lb[0].numel()),
 ]:
     ms = t(fn)
