@@ -138,9 +138,13 @@ size_t rv_yolo_ws_bytes(void* handle, int B);
 int rv_yolo_num_anchors(void* handle);
 /* Forward on B letterboxed u8 BGR images (B x in_h x in_w x 3).  raw_out
  * (nullable): the reference's raw prediction (B, 4+nc, A) f32 = cat(xywh *
- * stride, sigmoid(cls)).  cand (nullable): per image up to cand_cap NMS
- * candidate rows {x1,y1,x2,y2,score,cls,anchor,pad} (32 B) whose best class
- * score > conf, count in cand_n[B] (zeroed by this call). */
+ * stride, sigmoid(cls)).  cand (nullable): NMS candidate rows
+ * {x1,y1,x2,y2,score,cls,anchor,pad} (32 B) of every anchor whose best class
+ * score > conf, in the SEGMENTED layout: per image cand_cap rows, segment j
+ * (64 consecutive anchors of one head level, nseg = rv_yolo_cand_segments)
+ * owns rows [64 j, 64 j + cand_n[b * nseg + j]) in anchor order; cand_cap
+ * >= 64 * nseg.  No atomics, no pre-zeroing. */
+int rv_yolo_cand_segments(void* handle);
 int rv_yolo_forward(void* handle, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
                     float* raw_out, float conf, void* cand, int cand_cap, int* cand_n,
                     void* stream);
@@ -165,15 +169,23 @@ int rv_yolo_profile_read(void* handle, double* ms, double* flops, int* conv, int
 /* --- Ultralytics non_max_suppression + scale_boxes + class filter
  * (yolo_ultralytics.py:28-53), one workgroup per image. */
 size_t rv_nms_smem_bytes(void);
-/* scale5 = {gain (f32 of the python gain), pad_x, pad_y, clip_w, clip_h};
- * keep_mask4 (nullable = keep all): 128-bit class mask (classes_keep);
- * out: B x max_det x 6 {x1,y1,x2,y2,conf,cls} in score order, out_n[B]. */
-int rv_nms_postprocess(const void* cand, const int* cand_n, int B, int cap, float iou,
-                       int max_det, float max_wh, const float* scale5,
-                       const uint32_t* keep_mask4, float* out, int* out_n, void* stream);
-/* Candidate rows from a reference-layout raw prediction (B, 4+nc, A). */
+/* cand / seg_n: the segmented candidate layout of rv_yolo_forward (nseg
+ * segments of 64 rows, cap rows per image).  scale5 = {gain (f32 of the
+ * python gain), pad_x, pad_y, clip_w, clip_h}; keep_mask4 (nullable = keep
+ * all): 128-bit class mask (classes_keep); out: B x max_det x 6
+ * {x1,y1,x2,y2,conf,cls} in score order, out_n[B]; cand_total (nullable):
+ * candidates per image. */
+int rv_nms_postprocess(const void* cand, const int* seg_n, int B, int cap, int nseg,
+                       float iou, int max_det, float max_wh, const float* scale5,
+                       const uint32_t* keep_mask4, float* out, int* out_n, int* cand_total,
+                       void* stream);
+/* Segments of 64 anchors for a raw prediction with A anchors. */
+int rv_cand_segments(int A);
+/* Candidate rows from a reference-layout raw prediction (B, 4+nc, A), in the
+ * segmented layout (segment j = anchors [64 j, 64 j + 64)); cap >= 64 *
+ * rv_cand_segments(A). */
 int rv_candidates_from_raw(const float* raw, int B, int nc, int A, float conf, void* cand,
-                           int cap, int* cand_n, void* stream);
+                           int cap, int* seg_n, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Track: SortTracker.update (src/track/sort_tracker.py:212-278) batched over */

@@ -57,9 +57,12 @@ struct Cand {  // one detection candidate (Ultralytics NMS row before NMS)
 };
 
 // DFL + dist2bbox + sigmoid for all anchors.  Optionally writes the
-// reference's raw output (B, 4+nc, A) and appends every anchor whose best
-// class score > conf to cand[b][*] (count in cand_n[b], zeroed by caller).
+// reference's raw output (B, 4+nc, A) and every anchor whose best class
+// score > conf as a candidate row: segment j (64 consecutive anchors of one
+// level) fills cand[b][64 j ...] in anchor order, its count in
+// seg_n[b][j] (nseg = decode_segments()).
+int decode_segments(const HeadLevel* lv, int nlv);
 int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_max, float conf,
-                         float* raw, Cand* cand, int cand_cap, int* cand_n, hipStream_t s);
+                         float* raw, Cand* cand, int cand_cap, int* seg_n, hipStream_t s);
 
 }  // namespace rv

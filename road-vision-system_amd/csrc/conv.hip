@@ -284,10 +284,14 @@ struct PatchGeo {
 
 __device__ __forceinline__ int swz(int i) { return (i >> 2) & 3; }
 
+// bias: the lane's 4 channels per m-fragment, loaded once per block (a
+// global load in the epilogue would make the compiler wait vmcnt(0), i.e.
+// drain the next stage's LDS-DMA, before every tile's epilogue)
 template <int MR, int NR>
 __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[MR][NR], int cout0,
                                          const bool (&pv)[NR], const int (&pb)[NR],
-                                         const int (&py)[NR], const int (&px)[NR], int quad) {
+                                         const int (&py)[NR], const int (&px)[NR], int quad,
+                                         const f32x4 (&bias)[MR]) {
 #pragma unroll
   for (int n = 0; n < NR; ++n) {
     if (!pv[n]) continue;
@@ -298,11 +302,10 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[MR][NR]
       const int co = cout0 + m * 16 + quad * 4;
       if (co >= a.Cout) continue;
       float v[4];
-      const float4 bb = *(const float4*)(a.bias + co);
-      v[0] = acc[m][n][0] + bb.x;
-      v[1] = acc[m][n][1] + bb.y;
-      v[2] = acc[m][n][2] + bb.z;
-      v[3] = acc[m][n][3] + bb.w;
+      v[0] = acc[m][n][0] + bias[m][0];
+      v[1] = acc[m][n][1] + bias[m][1];
+      v[2] = acc[m][n][2] + bias[m][2];
+      v[3] = acc[m][n][3] + bias[m][3];
       if (a.act) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = silu(v[i]);
@@ -374,7 +377,7 @@ constexpr int patch_maxit() {
 // tile's first chunk -- streams in while step s runs on MFMA and while the
 // previous tile's epilogue stores drain.  Per-lane DMA offsets are computed
 // once per tile (no integer division in the chunk loop).
-template <int MR, int NR, int K, int S>
+template <int MR, int NR, int K, int S, bool BIG>
 __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int T2 = K * K;
@@ -424,6 +427,12 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
     woff[it] = (j < WJ && co < cout_pad) ? co * Kp + tap * cin_pad + q * 8 : -1;
   }
 
+  f32x4 bias[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    const int co = cout0 + m * 16 + quad * 4;  // bias is padded to Cout_pad16
+    bias[m] = co < cout_pad ? *(const f32x4*)(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   int poff[MAXP];
   uint32_t tailbad = 0;  // bit it: this lane's quarter is >= Cin in the last chunk
   const bf16_t* img = a.in;
@@ -533,7 +542,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
         px[n] = tx * g.C + ocol[n];
         pv[n] = oin[n] && py[n] < a.Ho && px[n] < a.Wo;
       }
-      epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad);
+      epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias);
       ti += gridDim.x;
       c = 0;
     } else {
@@ -589,11 +598,14 @@ static int num_cus() {
   return n;
 }
 
-template <int MR, int NR, int K, int S>
-static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, hipStream_t s) {
+// Launches needing more than the default 64 KB of dynamic LDS go to a
+// separate instantiation (BIG) whose cap is raised once: the cap is a
+// per-function attribute, and it is kept off the small-LDS launches.
+template <int MR, int NR, int K, int S, bool BIG>
+static int launch_patch_tb(const ConvArgs& a, const PatchGeo& g, size_t smem, hipStream_t s) {
   static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_patch_kernel<MR, NR, K, S>,
+  if (BIG && !attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)conv_patch_kernel<MR, NR, K, S, BIG>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) {
       (void)hipGetLastError();
@@ -609,8 +621,8 @@ static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, hip
   for (int i = 0; i < 8; ++i)
     if (occ_smem[i] == smem) occ = occ_val[i];
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_patch_kernel<MR, NR, K, S>, 256,
-                                                     smem) != hipSuccess || occ < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_patch_kernel<MR, NR, K, S, BIG>,
+                                                     256, smem) != hipSuccess || occ < 1)
       occ = 1;
     (void)hipGetLastError();
     for (int i = 0; i < 8; ++i)
@@ -627,8 +639,14 @@ static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, hip
   int gx = ntiles;
   if (persist) gx = std::min(ntiles, std::max(1, num_cus() * occ / ytiles));
   dim3 grid(gx, ytiles);
-  conv_patch_kernel<MR, NR, K, S><<<grid, 256, smem, s>>>(a, g);
+  conv_patch_kernel<MR, NR, K, S, BIG><<<grid, 256, smem, s>>>(a, g);
   return launch_status("conv_patch");
+}
+
+template <int MR, int NR, int K, int S>
+static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, hipStream_t s) {
+  if (smem > 64 * 1024) return launch_patch_tb<MR, NR, K, S, true>(a, g, smem, s);
+  return launch_patch_tb<MR, NR, K, S, false>(a, g, smem, s);
 }
 
 // stride-2 patches are ~4x the tile: only tiles whose offset registers and
@@ -975,7 +993,7 @@ int launch_sppf_pool(bf16_t* buf, int B, int H, int W, int c, hipStream_t s) {
     return RV_EINVAL;
   }
   static bool attr = false;
-  if (!attr) {
+  if (!attr && smem > 64 * 1024) {  // only raise the cap when a map needs it
     hipFuncSetAttribute((const void*)sppf_pool_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                         kSppfLds);
     (void)hipGetLastError();
@@ -1007,35 +1025,46 @@ template <int REG>
 __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B, int nc,
                                                             float conf, float* __restrict__ raw,
                                                             Cand* __restrict__ cand, int cap,
-                                                            int* __restrict__ cand_n) {
+                                                            int* __restrict__ seg_n) {
   extern __shared__ __attribute__((aligned(16))) float lg[];  // [64][cs + 4]
-  const int A = h.start[h.nlv];
   const int b = blockIdx.y;
-  // block -> (level, first anchor in level)
-  int blk = blockIdx.x, l = 0;
-  while (l + 1 < h.nlv && blk >= h.blk[l + 1]) ++l;
-  const HeadLevel& L = h.lv[l];
+  // block -> (level, first anchor in level).  Only compile-time indices
+  // into the by-value argument: a dynamic index would copy it to scratch.
+  const int blk = blockIdx.x;
+  int l = 0, A = h.start[1], lstart = 0, lblk = 0;
+  HeadLevel L = h.lv[0];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    if (i < h.nlv) A = h.start[i + 1];
+    if (i < h.nlv && blk >= h.blk[i]) {
+      l = i;
+      L = h.lv[i];
+      lstart = h.start[i];
+      lblk = h.blk[i];
+    }
+  }
+  (void)l;
   const int HW = L.H * L.W;
-  const int r0 = (blk - h.blk[l]) * 64;
+  const int r0 = (blk - lblk) * 64;
   const int na = min(64, HW - r0);
   const int tid = threadIdx.x;
   const int cs4 = L.cs / 4, ls4 = cs4 + 1;  // row length / LDS row stride in float4
-  const float4* src = (const float4*)(L.logits + ((size_t)b * HW + r0) * L.cs);
+  const f32x4* src = (const f32x4*)(L.logits + ((size_t)b * HW + r0) * L.cs);
   // 8 loads in flight per thread before any LDS store (a plain copy loop
   // would wait out one HBM latency per element)
   for (int i0 = tid; i0 < na * cs4; i0 += 8 * 256) {
-    float4 v[8];
+    f32x4 v[8];  // native vectors (a float4 struct array would live in scratch)
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = i0 + u * 256;
-      if (i < na * cs4) v[u] = src[i];
+      v[u] = i < na * cs4 ? src[i] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = i0 + u * 256;
       if (i < na * cs4) {
         const int row = i / cs4, c4 = i - (i / cs4) * cs4;
-        ((float4*)lg)[row * ls4 + c4] = v[u];
+        ((f32x4*)lg)[row * ls4 + c4] = v[u];
       }
     }
   }
@@ -1089,7 +1118,7 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
   const float d0 = __shfl(d, base), d1 = __shfl(d, base + 1), d2 = __shfl(d, base + 2),
               d3 = __shfl(d, base + 3);
   const int r = r0 + (live ? an : 0);
-  const int a = h.start[l] + r;
+  const int a = lstart + r;
   const int y = r / L.W, x = r - (r / L.W) * L.W;
   const float ax = (float)x + 0.5f, ay = (float)y + 0.5f;
   const float x1 = ax - d0, y1 = ay - d1, x2 = ax + d2, y2 = ay + d3;
@@ -1098,22 +1127,26 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
   if (raw && live) {
     for (int c = part; c < nc; c += 4)
       raw[((size_t)b * (4 + nc) + 4 + c) * A + a] = 1.0f / (1.0f + __expf(-pc[c]));
-    const float bx[4] = {cx, cy, w, hh};
-    raw[((size_t)b * (4 + nc) + part) * A + a] = bx[part];
+    const float bxv = part == 0 ? cx : (part == 1 ? cy : (part == 2 ? w : hh));
+    raw[((size_t)b * (4 + nc) + part) * A + a] = bxv;
   }
-  // one atomic per wave: ballot the passing anchors, the first of them
-  // reserves the wave's slots, lanes take their prefix rank
+  // Candidates go to this block's own 64-slot segment of the image's list
+  // (slot = segment * 64 + rank, ranks in anchor order) and the segment's
+  // count to seg_n: no cross-block atomics (same-address device atomics
+  // from thousands of waves serialise for ~100 us).
+  __shared__ int wcnt[4];
   const bool pass = live && part == 0 && cand && best > conf;
   const unsigned long long m = __ballot(pass);
-  if (m == 0ull) return;
-  const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-  const int lead = __ffsll((long long)m) - 1;
-  int base0 = 0;
-  if ((tid & 63) == lead) base0 = atomicAdd(&cand_n[b], __popcll(m));
-  base0 = __shfl(base0, lead);
+  const int wave = tid >> 6;
+  if ((tid & 63) == 0) wcnt[wave] = __popcll(m);
+  __syncthreads();
+  if (!cand) return;
+  int base0 = blk * 64;
+  for (int w2 = 0; w2 < wave; ++w2) base0 += wcnt[w2];
+  if (tid == 0) seg_n[(size_t)b * gridDim.x + blk] = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
   if (pass) {
-    const int i = base0 + rank;
+    const int i = base0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     if (i < cap) {
       const float hw = w / 2.0f, hh2 = hh / 2.0f;  // xywh2xyxy
       Cand c;
@@ -1128,6 +1161,12 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
       cand[(size_t)b * cap + i] = c;
     }
   }
+}
+
+int decode_segments(const HeadLevel* lv, int nlv) {
+  int n = 0;
+  for (int i = 0; i < nlv; ++i) n += ceil_div(lv[i].H * lv[i].W, 64);
+  return n;
 }
 
 int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_max, float conf,
@@ -1152,11 +1191,15 @@ int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_ma
   }
   const size_t smem = (size_t)64 * (cs + 4) * 4;
   static bool attr = false;
-  if (!attr) {
+  if (!attr && smem > 64 * 1024) {  // only raise the cap when the head needs it
     hipFuncSetAttribute((const void*)detect_decode_kernel<16>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();
     attr = true;
+  }
+  if (cand && cand_cap < h.blk[nlv] * 64) {
+    set_error("detect decode: cand_cap %d < %d segments x 64", cand_cap, h.blk[nlv]);
+    return RV_EINVAL;
   }
   detect_decode_kernel<16><<<dim3(h.blk[nlv], B), 256, smem, s>>>(h, B, nc, conf, raw, cand,
                                                                   cand_cap, cand_n);

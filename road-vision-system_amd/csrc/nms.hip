@@ -21,6 +21,7 @@ namespace rv {
 
 constexpr int kSortCap = 16384;  // candidates per image held in LDS (128 KB)
 constexpr int kMaxDet = 1024;
+constexpr int kMaxSeg = 1024;    // 64-candidate segments per image (<= 65536 slots)
 
 struct ScaleArgs {
   float gain;   // f32(gain) as torch divides by the python-float gain
@@ -51,10 +52,11 @@ __device__ __forceinline__ bool suppresses(float4 bi, float ai, float4 bj, float
 }
 
 __global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand,
-                                                   const int* __restrict__ cand_n, int cap,
+                                                   const int* __restrict__ seg_n, int nseg, int cap,
                                                    float max_wh, double iou, int max_det,
                                                    ScaleArgs sc, const uint32_t* __restrict__ keep4,
-                                                   float* __restrict__ out, int* __restrict__ out_n) {
+                                                   float* __restrict__ out, int* __restrict__ out_n,
+                                                   int* __restrict__ cand_total) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint64_t* keys = (uint64_t*)smem;                       // kSortCap
   float4* kbox = (float4*)(smem + kSortCap * 8);          // kept offset boxes (kMaxDet)
@@ -64,23 +66,51 @@ __global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand
   float* carea = (float*)(cbox + 64);                     // 64
   uint64_t* cmask = (uint64_t*)(carea + 64);              // 64
   __shared__ int s_nkeep;
+  __shared__ int wsum[16];
+  // exclusive prefix of the segment counts (+ total at [kMaxSeg]); aliases
+  // the kept-box array, which is only used after the sort
+  int* segoff = (int*)kbox;
+  static_assert((kMaxSeg + 1) * 4 <= kMaxDet * 16, "segoff alias");
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const Cand* cb = cand + (size_t)b * cap;
-  int n = cand_n[b];
-  if (n > cap) n = cap;
+  // segment counts -> exclusive prefix (one segment per thread, nseg <= 1024)
+  int cnt = 0;
+  if (tid < nseg) cnt = min(max(seg_n[(size_t)b * nseg + tid], 0), 64);
+  int incl = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_up(incl, off);
+    if ((tid & 63) >= off) incl += v;
+  }
+  if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+  __syncthreads();
+  int wpre = 0;
+  for (int w = 0; w < (tid >> 6); ++w) wpre += wsum[w];
+  if (tid < nseg) segoff[tid] = wpre + incl - cnt;
+  if (tid == 0) {
+    int tot = 0;
+    for (int w = 0; w < 16; ++w) tot += wsum[w];
+    segoff[kMaxSeg] = tot;
+  }
+  __syncthreads();
+  int n = segoff[kMaxSeg];
+  if (cand_total && tid == 0) cand_total[b] = n;
   if (n > kSortCap) n = kSortCap;  // capacity limit (documented in DESIGN.md)
   int np2 = 1;
   while (np2 < n) np2 <<= 1;
-  for (int i = tid; i < np2; i += blockDim.x) {
-    uint64_t k = ~0ull;
-    if (i < n) {
-      const Cand c = cb[i];
+  for (int i = tid; i < np2; i += blockDim.x) keys[i] = ~0ull;
+  __syncthreads();
+  for (int sl = tid; sl < nseg * 64; sl += blockDim.x) {
+    const int j = sl >> 6, k = sl & 63;
+    const int pos = segoff[j] + k;
+    const int next = j + 1 == nseg ? segoff[kMaxSeg] : segoff[j + 1];
+    if (pos < next && pos < n) {
+      const Cand c = cb[sl];
       const uint32_t sb = __float_as_uint(c.score);  // score > conf >= 0: bits are monotonic
-      k = ((uint64_t)(~sb) << 32) | ((uint64_t)(uint32_t)c.anchor << 16) | (uint64_t)i;
+      keys[pos] = ((uint64_t)(~sb) << 32) | ((uint64_t)(uint32_t)c.anchor << 16) | (uint64_t)sl;
     }
-    keys[i] = k;
   }
   __syncthreads();
   // bitonic sort ascending
@@ -184,28 +214,35 @@ __global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand
 }
 
 // Reference-layout candidates: raw (B, 4+nc, A) -> Cand rows (xc filter,
-// xywh2xyxy, best class), i.e. the first half of non_max_suppression.
-__global__ __launch_bounds__(256) void raw_candidates_kernel(const float* __restrict__ raw, int nc,
-                                                             int A, float conf,
-                                                             Cand* __restrict__ cand, int cap,
-                                                             int* __restrict__ cand_n) {
-  const int a = blockIdx.x * 256 + threadIdx.x;
+// xywh2xyxy, best class), i.e. the first half of non_max_suppression.  One
+// wave per 64-anchor segment, written in the segmented layout of
+// rv_nms_postprocess (slot = 64 * segment + rank in anchor order).
+__global__ __launch_bounds__(64) void raw_candidates_kernel(const float* __restrict__ raw, int nc,
+                                                            int A, float conf,
+                                                            Cand* __restrict__ cand, int cap,
+                                                            int* __restrict__ seg_n) {
+  const int j = blockIdx.x, lane = threadIdx.x;
+  const int a = j * 64 + lane;
   const int b = blockIdx.y;
-  if (a >= A) return;
   const float* r = raw + (size_t)b * (4 + nc) * A;
   float best = -INFINITY;
   int bc = 0;
-  for (int c = 0; c < nc; ++c) {
-    const float s = r[(size_t)(4 + c) * A + a];
-    if (s > best) {
-      best = s;
-      bc = c;
+  if (a < A)
+    for (int c = 0; c < nc; ++c) {
+      const float s = r[(size_t)(4 + c) * A + a];
+      if (s > best) {
+        best = s;
+        bc = c;
+      }
     }
-  }
-  if (!(best > conf)) return;
+  const bool pass = a < A && best > conf;
+  const unsigned long long m = __ballot(pass);
+  if (lane == 0) seg_n[(size_t)b * gridDim.x + j] = __popcll(m);
+  if (!pass) return;
+  const int i = j * 64 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
   const float cx = r[a], cy = r[(size_t)A + a], w = r[(size_t)2 * A + a], h = r[(size_t)3 * A + a];
   const float hw = w / 2.0f, hh = h / 2.0f;
-  const int i = atomicAdd(&cand_n[b], 1);
   if (i < cap) {
     Cand c;
     c.x1 = cx - hw;
@@ -228,12 +265,14 @@ extern "C" size_t rv_nms_smem_bytes(void) {
   return (size_t)kSortCap * 8 + (size_t)kMaxDet * (16 + 4 + 4) + 64 * (16 + 4 + 8);
 }
 
-extern "C" int rv_nms_postprocess(const void* cand, const int* cand_n, int B, int cap, float iou,
-                                  int max_det, float max_wh, const float* scale5,
+extern "C" int rv_nms_postprocess(const void* cand, const int* seg_n, int B, int cap, int nseg,
+                                  float iou, int max_det, float max_wh, const float* scale5,
                                   const uint32_t* keep_mask4, float* out, int* out_n,
-                                  void* stream) {
-  RV_CHECK_ARG(cand && cand_n && out && out_n && scale5, "null pointer");
+                                  int* cand_total, void* stream) {
+  RV_CHECK_ARG(cand && seg_n && out && out_n && scale5, "null pointer");
   RV_CHECK_ARG(B >= 0 && cap > 0 && cap <= 65536, "cap %d outside (0, 65536]", cap);
+  RV_CHECK_ARG(nseg > 0 && nseg <= kMaxSeg && nseg * 64 <= cap,
+               "nseg %d: need 0 < nseg <= %d and nseg * 64 <= cap %d", nseg, kMaxSeg, cap);
   RV_CHECK_ARG(max_det > 0 && max_det <= kMaxDet, "max_det %d outside (0, %d]", max_det, kMaxDet);
   if (B == 0) return RV_OK;
   ScaleArgs sc;
@@ -254,24 +293,21 @@ extern "C" int rv_nms_postprocess(const void* cand, const int* cand_n, int B, in
     }
     attr = true;
   }
-  nms_kernel<<<B, 1024, smem, as_stream(stream)>>>((const Cand*)cand, cand_n, cap, max_wh,
+  nms_kernel<<<B, 1024, smem, as_stream(stream)>>>((const Cand*)cand, seg_n, nseg, cap, max_wh,
                                                     (double)iou, max_det, sc, keep_mask4, out,
-                                                    out_n);
+                                                    out_n, cand_total);
   return launch_status("rv_nms_postprocess");
 }
 
+extern "C" int rv_cand_segments(int A) { return A > 0 ? ceil_div(A, 64) : 0; }
+
 extern "C" int rv_candidates_from_raw(const float* raw, int B, int nc, int A, float conf,
-                                      void* cand, int cap, int* cand_n, void* stream) {
-  RV_CHECK_ARG(raw && cand && cand_n, "null pointer");
-  RV_CHECK_ARG(B >= 0 && nc > 0 && A > 0 && A < 65536 && cap > 0, "bad raw shape");
+                                      void* cand, int cap, int* seg_n, void* stream) {
+  RV_CHECK_ARG(raw && cand && seg_n, "null pointer");
+  RV_CHECK_ARG(B >= 0 && nc > 0 && A > 0 && A < 65536 && cap >= ceil_div(A, 64) * 64,
+               "bad raw shape / cap < 64 * ceil(A / 64)");
   if (B == 0) return RV_OK;
-  hipStream_t s = as_stream(stream);
-  hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * B, s);
-  if (e != hipSuccess) {
-    set_error("memset: %s", hipGetErrorString(e));
-    return -(int)e;
-  }
-  raw_candidates_kernel<<<dim3(ceil_div(A, 256), B), 256, 0, s>>>(raw, nc, A, conf, (Cand*)cand,
-                                                                  cap, cand_n);
+  raw_candidates_kernel<<<dim3(ceil_div(A, 64), B), 64, 0, as_stream(stream)>>>(
+      raw, nc, A, conf, (Cand*)cand, cap, seg_n);
   return launch_status("rv_candidates_from_raw");
 }

@@ -116,30 +116,48 @@ __device__ void kf_predict(Track& t, double dt_raw) {
   t.P[48] += dt;
 }
 
-// 4x4 inverse, Gauss-Jordan with partial pivoting
+// 4x4 inverse, Gauss-Jordan with partial pivoting (first maximum |a[r][c]|).
+// Fully unrolled with compile-time row indices only (a pivot-indexed row
+// access would put the matrix in scratch memory).
 __device__ void inv4(const double* S, double* Si) {
   double a[4][8];
+#pragma unroll
   for (int i = 0; i < 4; ++i)
+#pragma unroll
     for (int j = 0; j < 8; ++j) a[i][j] = j < 4 ? S[i * 4 + j] : (j - 4 == i ? 1.0 : 0.0);
+#pragma unroll
   for (int c = 0; c < 4; ++c) {
     int p = c;
+    double best = fabs(a[c][c]);
+#pragma unroll
     for (int r = c + 1; r < 4; ++r)
-      if (fabs(a[r][c]) > fabs(a[p][c])) p = r;
-    if (p != c)
-      for (int j = 0; j < 8; ++j) {
-        const double tmp = a[c][j];
-        a[c][j] = a[p][j];
-        a[p][j] = tmp;
+      if (fabs(a[r][c]) > best) {
+        best = fabs(a[r][c]);
+        p = r;
       }
+#pragma unroll
+    for (int r = c + 1; r < 4; ++r)
+      if (p == r)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const double tmp = a[c][j];
+          a[c][j] = a[r][j];
+          a[r][j] = tmp;
+        }
     const double d = a[c][c];
+#pragma unroll
     for (int j = 0; j < 8; ++j) a[c][j] /= d;
+#pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (r == c) continue;
       const double f = a[r][c];
+#pragma unroll
       for (int j = 0; j < 8; ++j) a[r][j] -= f * a[c][j];
     }
   }
+#pragma unroll
   for (int i = 0; i < 4; ++i)
+#pragma unroll
     for (int j = 0; j < 4; ++j) Si[i * 4 + j] = a[i][j + 4];
 }
 

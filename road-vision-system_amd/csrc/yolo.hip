@@ -490,6 +490,17 @@ extern "C" size_t rv_yolo_ws_bytes(void* h, int B) {
 
 extern "C" int rv_yolo_num_anchors(void* h) { return h ? ((Model*)h)->nA : 0; }
 
+extern "C" int rv_yolo_cand_segments(void* h) {
+  if (!h) return 0;
+  const Model* M = (const Model*)h;
+  HeadLevel hl[3];
+  for (int i = 0; i < 3; ++i) {
+    hl[i].H = M->map_h[3 + i];
+    hl[i].W = M->map_w[3 + i];
+  }
+  return decode_segments(hl, 3);
+}
+
 extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
                                float* raw_out, float conf, void* cand, int cand_cap, int* cand_n,
                                void* stream) {
@@ -510,13 +521,6 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
     off = (off + b.elems_per_img * B * (b.f32 ? 4 : 2) + 255) & ~(size_t)255;
   }
   M->trace.clear();
-  if (cand_n) {
-    hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * B, E.s);
-    if (e != hipSuccess) {
-      set_error("memset: %s", hipGetErrorString(e));
-      return -(int)e;
-    }
-  }
   // backbone
   const ConvSpec& c0 = M->def.convs[0];
   int st = launch_conv0(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),

@@ -60,8 +60,11 @@ _SIGS = {
     "rv_yolo_profile": (c_int, [c_void_p, c_int]),
     "rv_yolo_profile_read": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
     "rv_nms_smem_bytes": (c_size_t, []),
-    "rv_nms_postprocess": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_int, c_float,
-                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rv_nms_postprocess": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int,
+                                   c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p]),
+    "rv_cand_segments": (c_int, [c_int]),
+    "rv_yolo_cand_segments": (c_int, [c_void_p]),
     "rv_candidates_from_raw": (c_int, [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int,
                                        c_void_p, c_void_p]),
     # track
@@ -108,7 +111,7 @@ def check(status: int, what: str = "") -> None:
         raise RVError(f"{what or 'rvhip'} failed with status {status}: {msg}")
 
 
-_NOCHECK = {"rv_abi_version", "rv_clahe_median_fits", "rv_clahe_median_letterbox_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
+_NOCHECK = {"rv_abi_version", "rv_cand_segments", "rv_yolo_cand_segments", "rv_clahe_median_fits", "rv_clahe_median_letterbox_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
             "rv_yolo_num_buffers", "rv_yolo_trace", "rv_yolo_profile_read"}
 
 

@@ -75,10 +75,15 @@ class YoloEngine:
         self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
         self.lb = torch.empty((self.max_batch, self.in_h, self.in_w, 3), dtype=torch.uint8,
                               device=dev)
-        self.cap = self.A
+        # segmented candidate layout: nseg segments of 64 rows per image
+        self.nseg = lib.rv_yolo_cand_segments(h)
+        self.cap = 64 * max(self.nseg, lib.rv_cand_segments(self.A))
         self.cand = torch.empty((self.max_batch, self.cap, CAND_BYTES // 4), dtype=torch.float32,
                                 device=dev)
-        self.cand_n = torch.zeros(self.max_batch, dtype=torch.int32, device=dev)
+        self.seg_n = torch.zeros((self.max_batch, max(self.nseg, lib.rv_cand_segments(self.A))),
+                                 dtype=torch.int32, device=dev)
+        self.cand_n = torch.zeros(self.max_batch, dtype=torch.int32, device=dev)  # set by NMS
+        self._nseg_cur = self.nseg
         self.dets = torch.zeros((self.max_batch, self.max_det, 6), dtype=torch.float32, device=dev)
         self.det_n = torch.zeros(self.max_batch, dtype=torch.int32, device=dev)
         gain, px, py = scale_boxes_params((self.in_h, self.in_w), (self.H, self.W))
@@ -109,21 +114,27 @@ class YoloEngine:
         lb = lb.contiguous()
         call("rv_yolo_forward", self._h, ptr(lb), B, ptr(self.ws), self.ws_bytes, ptr(raw),
              self.conf, ptr(self.cand) if candidates else None, self.cap,
-             ptr(self.cand_n) if candidates else None, stream_ptr())
+             ptr(self.seg_n) if candidates else None, stream_ptr())
+        self._nseg_cur = self.nseg
         return raw
 
     def nms(self, B: int):
-        call("rv_nms_postprocess", ptr(self.cand), ptr(self.cand_n), B, self.cap, self.iou,
-             self.max_det, self.max_wh, ptr(self.scale5), ptr(self.keep), ptr(self.dets),
-             ptr(self.det_n), stream_ptr())
+        call("rv_nms_postprocess", ptr(self.cand), ptr(self.seg_n), B, self.cap, self._nseg_cur,
+             self.iou, self.max_det, self.max_wh, ptr(self.scale5), ptr(self.keep), ptr(self.dets),
+             ptr(self.det_n), ptr(self.cand_n), stream_ptr())
         return self.dets[:B], self.det_n[:B]
 
     def nms_from_raw(self, raw: torch.Tensor):
         """Reference-layout entry (B, 4+nc, A) -> NMS (parity tests)."""
         B, C, A = raw.shape
         raw = raw.contiguous()
+        if self.seg_n.numel() < B * _lib.load().rv_cand_segments(A) or \
+                self.cap < 64 * _lib.load().rv_cand_segments(A):
+            raise ValueError(f"raw prediction with A={A} exceeds the candidate buffers")
+        self._nseg_cur = _lib.load().rv_cand_segments(A)
+        seg = self.seg_n.view(-1)[:B * self._nseg_cur].view(B, self._nseg_cur)
         call("rv_candidates_from_raw", ptr(raw), B, C - 4, A, self.conf, ptr(self.cand), self.cap,
-             ptr(self.cand_n), stream_ptr())
+             ptr(seg), stream_ptr())
         return self.nms(B)
 
     def run(self, frames: torch.Tensor):

@@ -172,6 +172,6 @@ def test_first_conv_sppf_and_decode(cuda):
     np.testing.assert_allclose(raw[:, :4], xywh, rtol=0, atol=2e-3)
     np.testing.assert_allclose(raw[:, 4:], 1 / (1 + np.exp(-y[:, 64:])), rtol=0, atol=1e-6)
     # candidates: every anchor with best score > conf, none else
-    n = int(eng.cand_n[0])
+    n = int(eng.seg_n.view(-1)[:eng.nseg].sum())  # image 0's segments
     expect = int((raw[0, 4:].max(0) > 0.25).sum())
     assert n == expect
