@@ -86,6 +86,8 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=int(os.environ.get("RV_CPU_FRAMES", 6)))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch kernels eagerly (no HIP graph)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="one graph per step; no overlap of step k's NMS+SORT with step k+1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -99,7 +101,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from rvs_amd import _lib
-    from rvs_amd.engine import RoadVisionEngine
+    from rvs_amd.engine import OverlappedSteps, RoadVisionEngine
     from rvs_amd.synth import road_frames
 
     cfg = bench_config()
@@ -114,24 +116,31 @@ def main():
         eng.step(frames[f], ts_all[f])
     torch.cuda.synchronize()
     lib = _lib.load()
-    graphs = None
-    if not args.eager:
+    graphs = runner = None
+    if not args.eager and not args.no_pipeline:
+        # the track stage of step k (NMS + SORT, latency-bound) overlaps the
+        # preprocess of step k+1 inside one graph (engine.OverlappedSteps)
+        runner = OverlappedSteps(eng, [frames[Wm + k] for k in range(K)],
+                                 [ts_all[Wm + k] for k in range(K)])
+        torch.cuda.synchronize()
+    elif not args.eager:
         # one HIP graph per timed step (its own frame batch); replayed in order
         graphs = [eng.capture(frames[Wm + k], ts_all[Wm + k])[0] for k in range(K)]
         torch.cuda.synchronize()
-        # captured steps advanced the tracker state: rewind to the post-warmup
-        # state is not needed for throughput, the replay re-runs every kernel.
     else:
         _lib.check(lib.rv_yolo_profile(eng.detector._h, K), "rv_yolo_profile")
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(K):
-        if graphs is not None:
-            graphs[k].replay()
-        else:
-            eng.step(frames[Wm + k], ts_all[Wm + k])
+    if runner is not None:
+        runner.run()
+    else:
+        for k in range(K):
+            if graphs is not None:
+                graphs[k].replay()
+            else:
+                eng.step(frames[Wm + k], ts_all[Wm + k])
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -142,7 +151,7 @@ def main():
 
     # live conv timing (HIP events on the launch stream): a separate eager
     # pass over the same K steps (event records cannot live inside graphs)
-    if graphs is not None:
+    if graphs is not None or runner is not None:
         _lib.check(lib.rv_yolo_profile(eng.detector._h, K), "rv_yolo_profile")
         for k in range(K):
             eng.step(frames[Wm + k], ts_all[Wm + k])
@@ -179,7 +188,10 @@ def main():
                                "CLAHE+Median (fused) -> letterbox -> YOLOv8n -> NMS -> SORT+homography",
                    "streams_per_gpu": S, "frame": [H, W], "detector_input": [eng.detector.in_h,
                                                                            eng.detector.in_w],
-                   "parallelism": f"streams sharded {S}/GPU, no collective"},
+                   "parallelism": f"streams sharded {S}/GPU, no collective",
+                   "execution": "eager" if args.eager else
+                                ("graph per step" if args.no_pipeline else
+                                 "graphs, NMS+SORT of step k overlapped with preprocess of step k+1")},
         "roofline": {
             "kernel": "conv_mfma (all YOLOv8n conv launches of a step, HIP events)",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16,

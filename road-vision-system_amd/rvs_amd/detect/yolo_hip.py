@@ -78,9 +78,11 @@ class YoloEngine:
         # segmented candidate layout: nseg segments of 64 rows per image
         self.nseg = lib.rv_yolo_cand_segments(h)
         self.cap = 64 * max(self.nseg, lib.rv_cand_segments(self.A))
-        self.cand = torch.empty((self.max_batch, self.cap, CAND_BYTES // 4), dtype=torch.float32,
+        # two candidate slots: a pipelined engine decodes frame k+1 into one
+        # slot while NMS still reads frame k's from the other
+        self.cand = torch.empty((2, self.max_batch, self.cap, CAND_BYTES // 4), dtype=torch.float32,
                                 device=dev)
-        self.seg_n = torch.zeros((self.max_batch, max(self.nseg, lib.rv_cand_segments(self.A))),
+        self.seg_n = torch.zeros((2, self.max_batch, max(self.nseg, lib.rv_cand_segments(self.A))),
                                  dtype=torch.int32, device=dev)
         self.cand_n = torch.zeros(self.max_batch, dtype=torch.int32, device=dev)  # set by NMS
         self._nseg_cur = self.nseg
@@ -107,34 +109,36 @@ class YoloEngine:
         return kernels.letterbox(frames, self.geo, out=self.lb[:B])
 
     def forward_raw(self, lb: torch.Tensor, raw: Optional[torch.Tensor] = None,
-                    candidates: bool = True):
+                    candidates: bool = True, slot: int = 0):
+        """YOLOv8 forward + decode; candidates go to candidate slot `slot`."""
         B = lb.shape[0]
         if B > self.max_batch:
             raise ValueError(f"batch {B} > max_batch {self.max_batch}")
         lb = lb.contiguous()
         call("rv_yolo_forward", self._h, ptr(lb), B, ptr(self.ws), self.ws_bytes, ptr(raw),
-             self.conf, ptr(self.cand) if candidates else None, self.cap,
-             ptr(self.seg_n) if candidates else None, stream_ptr())
+             self.conf, ptr(self.cand[slot]) if candidates else None, self.cap,
+             ptr(self.seg_n[slot]) if candidates else None, stream_ptr())
         self._nseg_cur = self.nseg
         return raw
 
-    def nms(self, B: int):
-        call("rv_nms_postprocess", ptr(self.cand), ptr(self.seg_n), B, self.cap, self._nseg_cur,
-             self.iou, self.max_det, self.max_wh, ptr(self.scale5), ptr(self.keep), ptr(self.dets),
-             ptr(self.det_n), ptr(self.cand_n), stream_ptr())
+    def nms(self, B: int, slot: int = 0):
+        """NMS + scale_boxes + class filter of candidate slot `slot`."""
+        call("rv_nms_postprocess", ptr(self.cand[slot]), ptr(self.seg_n[slot]), B, self.cap,
+             self._nseg_cur, self.iou, self.max_det, self.max_wh, ptr(self.scale5), ptr(self.keep),
+             ptr(self.dets), ptr(self.det_n), ptr(self.cand_n), stream_ptr())
         return self.dets[:B], self.det_n[:B]
 
     def nms_from_raw(self, raw: torch.Tensor):
         """Reference-layout entry (B, 4+nc, A) -> NMS (parity tests)."""
         B, C, A = raw.shape
         raw = raw.contiguous()
-        if self.seg_n.numel() < B * _lib.load().rv_cand_segments(A) or \
+        if self.seg_n[0].numel() < B * _lib.load().rv_cand_segments(A) or \
                 self.cap < 64 * _lib.load().rv_cand_segments(A):
             raise ValueError(f"raw prediction with A={A} exceeds the candidate buffers")
         self._nseg_cur = _lib.load().rv_cand_segments(A)
-        seg = self.seg_n.view(-1)[:B * self._nseg_cur].view(B, self._nseg_cur)
-        call("rv_candidates_from_raw", ptr(raw), B, C - 4, A, self.conf, ptr(self.cand), self.cap,
-             ptr(seg), stream_ptr())
+        seg = self.seg_n[0].view(-1)[:B * self._nseg_cur].view(B, self._nseg_cur)
+        call("rv_candidates_from_raw", ptr(raw), B, C - 4, A, self.conf, ptr(self.cand[0]),
+             self.cap, ptr(seg), stream_ptr())
         return self.nms(B)
 
     def run(self, frames: torch.Tensor):

@@ -60,18 +60,37 @@ class RoadVisionEngine:
         # default chain: CLAHE + median + the detector's LetterBox in one pass
         self.fused_letterbox = self.pipeline.letterbox_fusable(self.H, self.W, self.detector.geo)
 
+    def preprocess_stage(self, frames: torch.Tensor):
+        """pipeline(raw) + the detector's LetterBox (main_preview.py:94-99)
+        for (S,H,W,3) u8 device frames -> (proc, letterboxed batch)."""
+        if self.fused_letterbox:
+            return self.pipeline.run_with_letterbox(frames, self.detector.geo,
+                                                    self.detector.lb[:frames.shape[0]])
+        proc = self.pipeline(frames)
+        return proc, self.detector.letterbox(proc)
+
+    def yolo_stage(self, lb: torch.Tensor, slot: int = 0) -> None:
+        """YOLOv8 forward + decode; NMS candidates land in candidate slot `slot`."""
+        self.detector.forward_raw(lb, slot=slot)
+
+    def detect_stage(self, frames: torch.Tensor, slot: int = 0) -> torch.Tensor:
+        proc, lb = self.preprocess_stage(frames)
+        self.yolo_stage(lb, slot)
+        return proc
+
+    def track_stage(self, ts: torch.Tensor, slot: int = 0) -> Dict[str, torch.Tensor]:
+        """NMS of candidate slot `slot` + SORT/geometry (main_preview.py:99-109)."""
+        dets, det_n = self.detector.nms(ts.shape[0], slot)
+        tid, dist, spd = self.tracker.update(dets, det_n, ts)
+        return {"dets": dets, "det_n": det_n, "track_id": tid, "distance_m": dist,
+                "speed_kmh": spd}
+
     def step(self, frames: torch.Tensor, ts: torch.Tensor) -> Dict[str, torch.Tensor]:
         """frames (S,H,W,3) u8 on device, ts (S,) f64 on device."""
-        if self.fused_letterbox:
-            proc, lb = self.pipeline.run_with_letterbox(frames, self.detector.geo,
-                                                        self.detector.lb[:frames.shape[0]])
-            dets, det_n = self.detector.run_letterboxed(lb)
-        else:
-            proc = self.pipeline(frames)
-            dets, det_n = self.detector.run(proc)
-        tid, dist, spd = self.tracker.update(dets, det_n, ts)
-        return {"proc": proc, "dets": dets, "det_n": det_n, "track_id": tid,
-                "distance_m": dist, "speed_kmh": spd}
+        proc = self.detect_stage(frames, 0)
+        out = self.track_stage(ts, 0)
+        out["proc"] = proc
+        return out
 
     def capture(self, frames: torch.Tensor, ts: torch.Tensor):
         """Record one step on (frames, ts) -- fixed device buffers -- into a
@@ -109,3 +128,46 @@ class RoadVisionEngine:
 
     def close(self):
         self.detector.close()
+
+
+
+class OverlappedSteps:
+    """K captured steps whose latency-bound tail overlaps the next step's head.
+
+    The track stage of a step (NMS + SORT: one workgroup per frame / camera
+    stream, so it leaves most of the 256 CUs idle) has no data dependence on
+    the next step's preprocess (CLAHE + median + letterbox of new frames), so
+    graph j runs  [track(j-1) on a side stream  ||  preprocess(j)]  -> join ->
+    yolo(j).  The convs never share the device with another kernel.  Graph 0
+    is preprocess(0) + yolo(0), a last graph runs track(K-1); the two NMS
+    candidate slots alternate by step.  Replayed in order, the K steps give the
+    same results as K step() calls (tests/test_engine_gpu.py)."""
+
+    def __init__(self, eng: "RoadVisionEngine", frames, ts):
+        self.eng = eng
+        K = len(frames)
+        side = torch.cuda.Stream(eng.device)
+        self.graphs = []
+        self.outs = []
+        for j in range(K + 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                cur = torch.cuda.current_stream()
+                if j > 0:
+                    side.wait_stream(cur)
+                    with torch.cuda.stream(side):
+                        out = eng.track_stage(ts[j - 1], (j - 1) % 2)
+                if j < K:
+                    proc, lb = eng.preprocess_stage(frames[j])
+                if j > 0:
+                    cur.wait_stream(side)
+                    out["proc"] = self._proc
+                    self.outs.append(out)
+                if j < K:
+                    eng.yolo_stage(lb, j % 2)
+                    self._proc = proc
+            self.graphs.append(g)
+
+    def run(self):
+        for g in self.graphs:
+            g.replay()

@@ -49,3 +49,41 @@ def test_engine_steps_match_oracle(cuda):
             assert [d.track_id for d in res[s]] == [d.track_id for d in dets]
             assert [d.distance_m for d in res[s]] == [d.distance_m for d in dets]
     eng.close()
+
+
+def test_overlapped_steps_match_sequential_steps(cuda):
+    """bench.py's timed mode (engine.OverlappedSteps): the track stage of step
+    k runs on a side stream beside the preprocess of step k+1.  The final
+    detections, track ids, proc frames and the whole SORT state must equal
+    those of plain sequential step() calls."""
+    from rvs_amd.config import load_config
+    from rvs_amd.engine import OverlappedSteps, RoadVisionEngine
+    from rvs_amd.synth import road_frames
+    cfg = load_config()
+    cfg["geometry"]["enabled"] = True
+    cfg["geometry"]["projector"]["image_points"] = IMG
+    cfg["geometry"]["projector"]["world_points"] = WLD
+    S, H, W, F = 4, 1080, 1920, 6
+    frames = road_frames(S, F, H, W, device=cuda)
+    ts = torch.tensor([[f / 30.0] * S for f in range(F)], dtype=torch.float64, device=cuda)
+    seq = RoadVisionEngine(cfg, S, (H, W), device=cuda)
+    for f in range(F):
+        out_seq = seq.step(frames[f], ts[f])
+    ovl = RoadVisionEngine(cfg, S, (H, W), device=cuda)
+    ovl.step(frames[0], ts[0])  # eager first step (one-time kernel setup)
+    run = OverlappedSteps(ovl, [frames[f] for f in range(1, F)], [ts[f] for f in range(1, F)])
+    run.run()
+    torch.cuda.synchronize()
+    r_seq, r_ovl = seq.results(out_seq), ovl.results(run.outs[-1])
+    key = lambda r: [[(d.x1, d.y1, d.x2, d.y2, d.conf, d.cls_id, d.track_id, d.distance_m,  # noqa
+                       d.speed_kmh) for d in s] for s in r]
+    assert key(r_seq) == key(r_ovl)
+    np.testing.assert_array_equal(run.outs[-1]["proc"].cpu().numpy(), out_seq["proc"].cpu().numpy())
+    Ts, xs, ms = seq.tracker.export()
+    To, xo, mo = ovl.tracker.export()
+    np.testing.assert_array_equal(Ts, To)
+    for s in range(S):
+        np.testing.assert_array_equal(xs[s, :Ts[s]], xo[s, :To[s]])
+        np.testing.assert_array_equal(ms[s, :Ts[s]], mo[s, :To[s]])
+    seq.close()
+    ovl.close()

@@ -44,5 +44,5 @@ for i in range(n):
     tot += t
     rows.append((t, name, ci, co, k, st, fl[i]))
 print(f"B={B} {H}x{W} forward {fwd:.3f} ms (events), conv sum {tot:.3f} ms over {len(rows)} launches")
-for t, name, ci, co, k, st, f in sorted(rows, reverse=True)[:40]:
+for t, name, ci, co, k, st, f in (rows if os.environ.get("ORDER") else sorted(rows, reverse=True)[:40]):
     print(f"{t*1e3:8.1f} us {f/1e9:7.2f} GF {f/t/1e9:7.1f} TF/s  {name:22s} {ci:4d}->{co:4d} k{k} s{st}")
