@@ -166,6 +166,19 @@ int rv_yolo_trace(void* handle, int* recs, int max_recs);
 int rv_yolo_profile(void* handle, int max_forwards);
 int rv_yolo_profile_read(void* handle, double* ms, double* flops, int* conv, int n);
 
+/* Per-layer autotuning of the conv kernels (no reference counterpart: it
+ * picks, per conv launch of this handle's forward, the fastest of the valid
+ * LDS-staged kernel configurations on the given letterboxed batch; later
+ * forwards use the choices).  Synchronous, not graph-capturable; call once
+ * after rv_yolo_create.  verify != 0: every configuration's output is also
+ * compared with the default's (they are bit-identical by construction) and
+ * *n_bad counts the ones that were not.  reps: timed launches per config. */
+int rv_yolo_autotune(void* handle, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
+                     int reps, int verify, int* n_bad, void* stream);
+/* cfg5 = {MR, NR, G, resw, persist} of conv launch idx (MR 0 = default
+ * heuristic); returns the number of tuned launches (0 before autotuning). */
+int rv_yolo_tuned_config(void* handle, int idx, int* cfg5);
+
 /* --- Ultralytics non_max_suppression + scale_boxes + class filter
  * (yolo_ultralytics.py:28-53), one workgroup per image. */
 size_t rv_nms_smem_bytes(void);

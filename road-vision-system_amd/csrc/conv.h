@@ -30,10 +30,31 @@ struct ConvArgs {
   const bf16_t* res;
   int res_cs, res_co;
   int act;  // 1: SiLU
+  // optional second group (a block-diagonal conv: the Detect head's
+  // parallel cv2 / cv3 branches in one launch).  Output channels
+  // [g2_cout0, Cout) read input channels [g2_in_co, g2_in_co + g2_Cin) of
+  // the same input buffer with their own packed weights and bias; output
+  // channel g2_cout0 + j is that group's channel j.  g2_cout0 = 0: one group.
+  int g2_cout0, g2_in_co, g2_Cin;
+  const bf16_t* g2_w;
+  const float* g2_bias;
 };
 
-// Implicit-GEMM conv on MFMA (v_mfma_f32_16x16x32_bf16).
+// One configuration of the LDS-staged conv kernel: MR x NR 16x16 fragments
+// per wave, G input-channel chunks (32 ch) per pipeline stage, resident
+// weights, persistent grid.
+struct ConvCfg {
+  int mr, nr, G, resw, persist;
+};
+
+// Implicit-GEMM conv on MFMA (v_mfma_f32_16x16x32_bf16), default config.
 int launch_conv(const ConvArgs& a, hipStream_t s);
+// The same with an explicit configuration; whether a configuration is valid
+// for a layer; the valid configurations of a layer (the autotuner's search
+// space: returns the count, fills at most cap).
+int launch_conv_cfg(const ConvArgs& a, const ConvCfg& c, hipStream_t s);
+bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c);
+int conv_candidates(const ConvArgs& a, ConvCfg* out, int cap);
 
 // First conv (3 -> C0, k3 s2 p1) straight from the u8 BGR letterboxed
 // frame, f32 arithmetic: x = u8/255 with the RGB order of the reference

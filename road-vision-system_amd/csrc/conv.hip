@@ -221,6 +221,11 @@ static int try_launch_patch(const ConvArgs& a, hipStream_t s, int* st);
 int launch_conv(const ConvArgs& a, hipStream_t s) {
   int st = 0;
   if (try_launch_patch(a, s, &st)) return st;
+  if (a.g2_cout0 > 0) {
+    set_error("grouped conv (Cout %d, split %d) has no patch-kernel configuration", a.Cout,
+              a.g2_cout0);
+    return RV_EINVAL;
+  }
   const int T = (a.Cout + 15) / 16;
   const long M = (long)a.B * a.Ho * a.Wo;
   struct Cand {
@@ -276,6 +281,7 @@ __device__ __attribute__((aligned(64))) uint4 g_zero16[4];
 
 struct PatchGeo {
   int C, R;        // output tile cols / rows (R*C <= 64*NR)
+  int G;           // input-channel chunks per pipeline stage
   int PH, PW;      // input patch rows / cols
   int pinst;       // DMA instructions for the patch (64 x 16-B slots each)
   int tiles_x, tiles_y;
@@ -372,12 +378,21 @@ constexpr int patch_maxit() {
 }
 
 // Persistent, software-pipelined form: the block owns cout tile blockIdx.y
-// and walks pixel tiles blockIdx.x, +gridDim.x, ...; the (tile, chunk)
-// steps are flattened so the DMA of step s+1 -- the next chunk or the next
-// tile's first chunk -- streams in while step s runs on MFMA and while the
-// previous tile's epilogue stores drain.  Per-lane DMA offsets are computed
-// once per tile (no integer division in the chunk loop).
-template <int MR, int NR, int K, int S, bool BIG>
+// and walks pixel tiles blockIdx.x, +gridDim.x, ...  A step is (tile, group
+// of G input-channel chunks); the DMA of step s+1 -- the next group or the
+// next tile's first group -- streams in while step s runs on MFMA and while
+// the previous tile's epilogue stores drain.  G > 1 cuts the number of
+// dependent DMA round trips per tile (a deep-K layer with few tiles is a
+// chain of nch / G latencies, not nch).  RESW: the block's whole weight slab
+// (nch chunks) is DMA'd into LDS once at kernel start and stays resident, so
+// a step only moves its input patch.  Per-lane DMA offsets are computed once
+// per tile (no integer division in the chunk loop).
+//
+// Grouped form (ConvArgs::g2_*): cout tiles at or above g2_cout0 read their
+// own input channel slice / weights / bias (a block-diagonal conv: the
+// Detect head's cv2 and cv3 branches in one launch).  The host keeps every
+// tile inside one group.
+template <int MR, int NR, int K, int S, bool RESW>
 __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int T2 = K * K;
@@ -387,20 +402,37 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
   static_assert(MAXP <= 32, "tail mask is 32 bits");
   constexpr int WJ = BC * T2 / 16;            // weight DMA instructions per chunk
   constexpr int MAXW = (WJ + 3) / 4;
-  const int stage_bytes = g.p_bytes + W_BYTES;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int col = lane & 15, quad = lane >> 4;
-  const int cout0 = blockIdx.y * BC;
-  const int cout_pad = (a.Cout + 15) & ~15;
-  const int cin_pad = (a.Cin + 31) & ~31;
+  const int cout0 = blockIdx.y * BC;  // first output channel of the tile (output numbering)
+  // the tile's group: its input slice, weights, bias and weight row base wc0
+  int wc0 = cout0, gcout = a.g2_cout0 > 0 ? a.g2_cout0 : a.Cout;
+  int in_co = a.in_co, Cin = a.Cin;
+  const bf16_t* wts = a.w;
+  const float* bias_p = a.bias;
+  if (a.g2_cout0 > 0 && cout0 >= a.g2_cout0) {
+    wc0 = cout0 - a.g2_cout0;
+    gcout = a.Cout - a.g2_cout0;
+    in_co = a.g2_in_co;
+    Cin = a.g2_Cin;
+    wts = a.g2_w;
+    bias_p = a.g2_bias;
+  }
+  const int wcout_pad = (gcout + 15) & ~15;
+  const int cin_pad = (Cin + 31) & ~31;
   const int Kp = T2 * cin_pad;
   const int nch = cin_pad >> 5;
+  const int G = g.G < nch ? g.G : nch;
+  const int ngrp = (nch + G - 1) / G;
+  const int chunk_bytes = g.p_bytes + (RESW ? 0 : W_BYTES);
+  const int stage_bytes = G * chunk_bytes;
+  uint8_t* const stages = smem + (RESW ? nch * W_BYTES : 0);
   constexpr int pad = K / 2;
   const int tiles_img = g.tiles_x * g.tiles_y;
   const int ntiles = a.B * tiles_img;
   const int my_tiles = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int nsteps = my_tiles * nch;
+  const int nsteps = my_tiles * ngrp;
   const int npp = g.PH * g.PW;
   const float inv_pw = 1.0f / (float)g.PW;
 
@@ -415,23 +447,11 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
     oin[n] = q < g.R * g.C;
     pb80[n] = (oin[n] ? (orow[n] * S) * g.PW + ocol[n] * S : 0) * kPixB + quad * 16;
   }
-  // block-constant: weight DMA offsets (chunk 0) per instruction
-  int woff[MAXW];
-#pragma unroll
-  for (int it = 0; it < MAXW; ++it) {
-    const int j = wave + 4 * it;
-    const int pr = j * 16 + (lane >> 2);
-    const int row = pr / T2, tap = pr - (pr / T2) * T2;
-    const int q = (lane & 3) ^ swz(row);
-    const int co = cout0 + row;
-    woff[it] = (j < WJ && co < cout_pad) ? co * Kp + tap * cin_pad + q * 8 : -1;
-  }
-
   f32x4 bias[MR];
 #pragma unroll
   for (int m = 0; m < MR; ++m) {
-    const int co = cout0 + m * 16 + quad * 4;  // bias is padded to Cout_pad16
-    bias[m] = co < cout_pad ? *(const f32x4*)(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int co = wc0 + m * 16 + quad * 4;  // bias is padded to Cout_pad16
+    bias[m] = co < wcout_pad ? *(const f32x4*)(bias_p + co) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   int poff[MAXP];
   uint32_t tailbad = 0;  // bit it: this lane's quarter is >= Cin in the last chunk
@@ -441,7 +461,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
     const int r = ti - b * tiles_img;
     const int ty = r / g.tiles_x, tx = r - (r / g.tiles_x) * g.tiles_x;
     const int iy0 = ty * g.R * S - pad, ix0 = tx * g.C * S - pad;
-    img = a.in + (size_t)b * a.Hin * a.Win * a.in_cs + a.in_co;
+    img = a.in + (size_t)b * a.Hin * a.Win * a.in_cs + in_co;
     tailbad = 0;
 #pragma unroll
     for (int it = 0; it < MAXP; ++it) {
@@ -453,82 +473,101 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
       const bool ok = q < 4 && pix < npp && (unsigned)iy < (unsigned)a.Hin &&
                       (unsigned)ix < (unsigned)a.Win;
       poff[it] = ok ? (iy * a.Win + ix) * a.in_cs + q * 8 : -1;
-      if ((nch - 1) * 32 + q * 8 >= a.Cin) tailbad |= 1u << it;
+      if ((nch - 1) * 32 + q * 8 >= Cin) tailbad |= 1u << it;
     }
   };
-  auto stage = [&](int c, int buf) {
-    uint8_t* P = smem + buf * stage_bytes;
-    uint8_t* Wl = P + g.p_bytes;
-    const uint32_t bad = c == nch - 1 ? tailbad : 0u;
-#pragma unroll
-    for (int it = 0; it < MAXP; ++it) {
-      const int j = wave + 4 * it;
-      if (j < g.pinst) {
-        const void* src = (poff[it] >= 0 && !((bad >> it) & 1))
-                              ? (const void*)(img + poff[it] + c * 32)
-                              : (const void*)g_zero16;
-        __builtin_amdgcn_global_load_lds(src, (void*)(P + j * 1024), 16, 0, 0);
-      }
-    }
+  // weight DMA: instruction j moves (row, tap) pairs 16 j .. 16 j + 15, a
+  // quarter (8 channels of chunk c) per lane; offsets are recomputed per
+  // call (constant divisor, no registers held across the loop)
+  auto dma_weights = [&](int c, uint8_t* Wl) {
 #pragma unroll
     for (int it = 0; it < MAXW; ++it) {
       const int j = wave + 4 * it;
       if (j < WJ) {
-        const void* src = woff[it] >= 0 ? (const void*)(a.w + woff[it] + c * 32)
-                                        : (const void*)g_zero16;
+        const int pr = j * 16 + (lane >> 2);
+        const int row = pr / T2, tap = pr - (pr / T2) * T2;
+        const int q = (lane & 3) ^ swz(row);
+        const int co = wc0 + row;
+        const void* src = co < wcout_pad ? (const void*)(wts + co * Kp + tap * cin_pad + q * 8 + c * 32)
+                                         : (const void*)g_zero16;
         __builtin_amdgcn_global_load_lds(src, (void*)(Wl + j * 1024), 16, 0, 0);
       }
     }
   };
-  f32x4 acc[MR][NR];
-  auto compute = [&](int buf) {
-    const uint8_t* P = smem + buf * stage_bytes;
-    const uint8_t* Wl = P + g.p_bytes;
+  auto stage = [&](int grp, int buf) {
+    for (int gi = 0; gi < G; ++gi) {
+      const int c = grp * G + gi;
+      if (c >= nch) break;
+      uint8_t* P = stages + buf * stage_bytes + gi * chunk_bytes;
+      const uint32_t bad = c == nch - 1 ? tailbad : 0u;
 #pragma unroll
-    for (int ky = 0; ky < K; ++ky) {
-      const uint8_t* Prow = P + ky * g.PW * kPixB;
-#pragma unroll
-      for (int kx = 0; kx < K; ++kx) {
-        const int tap = ky * K + kx;
-        bf16x8 A[MR], Bf[NR];
-#pragma unroll
-        for (int m = 0; m < MR; ++m) {
-          const int row = m * 16 + col;
-          A[m] = __builtin_bit_cast(
-              bf16x8, *(const uint4*)(Wl + (row * T2 + tap) * 64 + ((quad ^ swz(row)) << 4)));
+      for (int it = 0; it < MAXP; ++it) {
+        const int j = wave + 4 * it;
+        if (j < g.pinst) {
+          const void* src = (poff[it] >= 0 && !((bad >> it) & 1))
+                                ? (const void*)(img + poff[it] + c * 32)
+                                : (const void*)g_zero16;
+          __builtin_amdgcn_global_load_lds(src, (void*)(P + j * 1024), 16, 0, 0);
         }
+      }
+      if constexpr (!RESW) dma_weights(c, P + g.p_bytes);
+    }
+  };
+  f32x4 acc[MR][NR];
+  auto compute = [&](int grp, int buf) {
+    for (int gi = 0; gi < G; ++gi) {
+      const int c = grp * G + gi;
+      if (c >= nch) break;
+      const uint8_t* P = stages + buf * stage_bytes + gi * chunk_bytes;
+      const uint8_t* Wl = RESW ? smem + c * W_BYTES : P + g.p_bytes;
 #pragma unroll
-        for (int n = 0; n < NR; ++n)
-          Bf[n] = __builtin_bit_cast(bf16x8, *(const uint4*)(Prow + pb80[n] + kx * kPixB));
+      for (int ky = 0; ky < K; ++ky) {
+        const uint8_t* Prow = P + ky * g.PW * kPixB;
 #pragma unroll
-        for (int m = 0; m < MR; ++m)
+        for (int kx = 0; kx < K; ++kx) {
+          const int tap = ky * K + kx;
+          bf16x8 A[MR], Bf[NR];
+#pragma unroll
+          for (int m = 0; m < MR; ++m) {
+            const int row = m * 16 + col;
+            A[m] = __builtin_bit_cast(
+                bf16x8, *(const uint4*)(Wl + (row * T2 + tap) * 64 + ((quad ^ swz(row)) << 4)));
+          }
 #pragma unroll
           for (int n = 0; n < NR; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[m], Bf[n], acc[m][n], 0, 0, 0);
+            Bf[n] = __builtin_bit_cast(bf16x8, *(const uint4*)(Prow + pb80[n] + kx * kPixB));
+#pragma unroll
+          for (int m = 0; m < MR; ++m)
+#pragma unroll
+            for (int n = 0; n < NR; ++n)
+              acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[m], Bf[n], acc[m][n], 0, 0, 0);
+        }
       }
     }
   };
 
   if (nsteps == 0) return;
   int ti = blockIdx.x;  // tile of the current step
-  int c = 0;            // chunk of the current step
+  int grp = 0;          // chunk group of the current step
+  if constexpr (RESW)
+    for (int c = 0; c < nch; ++c) dma_weights(c, smem + c * W_BYTES);
   prep_tile(ti);
   stage(0, 0);
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
-    if (c == 0) {
+    if (grp == 0) {
 #pragma unroll
       for (int m = 0; m < MR; ++m)
 #pragma unroll
         for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     // issue step s+1
-    const bool last = c + 1 == nch;
+    const bool last = grp + 1 == ngrp;
     if (s + 1 < nsteps) {
       if (last) prep_tile(ti + gridDim.x);
-      stage(last ? 0 : c + 1, (s + 1) & 1);
+      stage(last ? 0 : grp + 1, (s + 1) & 1);
     }
-    compute(s & 1);
+    compute(grp, s & 1);
     if (last) {
       const int b = ti / tiles_img;
       const int r = ti - b * tiles_img;
@@ -544,25 +583,33 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
       }
       epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias);
       ti += gridDim.x;
-      c = 0;
+      grp = 0;
     } else {
-      ++c;
+      ++grp;
     }
     __syncthreads();
   }
 }
 
-static bool patch_geo(const ConvArgs& a, int NR, int MR, PatchGeo& g, size_t& smem) {
+// Input-channel chunks (32 channels) of the larger group.
+static int conv_nch(const ConvArgs& a) {
+  int cin = a.Cin;
+  if (a.g2_cout0 > 0 && a.g2_Cin > cin) cin = a.g2_Cin;
+  return (cin + 31) / 32;
+}
+
+static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& smem) {
   if (!((a.k == 1 || a.k == 3) && (a.stride == 1 || a.stride == 2) && a.pad == a.k / 2)) return false;
+  const int NR = c.nr, MR = c.mr;
   const int P = 64 * NR;
   int C;
   if (a.Wo <= P && a.Wo <= 64) {
     C = a.Wo;
   } else {
     C = 16;
-    for (int c : {64, 32, 16})
-      if (c <= P && a.Wo % c == 0) {
-        C = c;
+    for (int cc : {64, 32, 16})
+      if (cc <= P && a.Wo % cc == 0) {
+        C = cc;
         break;
       }
     if (a.Wo % C != 0) C = P >= 32 ? 32 : 16;
@@ -576,11 +623,14 @@ static bool patch_geo(const ConvArgs& a, int NR, int MR, PatchGeo& g, size_t& sm
   g.p_bytes = g.pinst * 1024;
   g.tiles_x = ceil_div(a.Wo, g.C);
   g.tiles_y = ceil_div(a.Ho, g.R);
+  const int nch = conv_nch(a);
+  g.G = std::max(1, std::min(c.G, nch));
   // per-lane offset registers of the kernel (patch_maxit)
   const int maxit = (a.stride == 2 ? 6 : 3) * NR + 2;
   if (ceil_div(g.pinst, 4) > maxit) return false;
-  // two stages: the next (tile, chunk) streams in during the current one
-  smem = 2 * ((size_t)g.p_bytes + (size_t)16 * MR * a.k * a.k * 64);
+  const size_t wb = (size_t)16 * MR * a.k * a.k * 64;
+  // two stages: the next (tile, chunk group) streams in during the current one
+  smem = (c.resw ? nch * wb : 0) + 2 * (size_t)g.G * (g.p_bytes + (c.resw ? 0 : wb));
   return smem <= 160 * 1024;
 }
 
@@ -598,15 +648,16 @@ static int num_cus() {
   return n;
 }
 
-// Launches needing more than the default 64 KB of dynamic LDS go to a
-// separate instantiation (BIG) whose cap is raised once: the cap is a
-// per-function attribute, and it is kept off the small-LDS launches.
-template <int MR, int NR, int K, int S, bool BIG>
-static int launch_patch_tb(const ConvArgs& a, const PatchGeo& g, size_t smem, hipStream_t s) {
+// Every instantiation gets the full 160 KB dynamic-LDS cap once; resident
+// blocks per CU are cached per LDS size (per instantiation).
+template <int MR, int NR, int K, int S, bool RESW>
+static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, int persist,
+                          hipStream_t s) {
   static bool attr = false;
-  if (BIG && !attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_patch_kernel<MR, NR, K, S, BIG>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  auto fn = conv_patch_kernel<MR, NR, K, S, RESW>;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024);
     if (e != hipSuccess) {
       (void)hipGetLastError();
       set_error("hipFuncSetAttribute: %s", hipGetErrorString(e));
@@ -614,39 +665,30 @@ static int launch_patch_tb(const ConvArgs& a, const PatchGeo& g, size_t smem, hi
     }
     attr = true;
   }
-  // resident blocks per CU at this LDS size (cached per size)
-  static size_t occ_smem[8] = {0};
-  static int occ_val[8] = {0};
+  static size_t occ_smem[16] = {0};
+  static int occ_val[16] = {0};
   int occ = 0;
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 16; ++i)
     if (occ_smem[i] == smem) occ = occ_val[i];
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_patch_kernel<MR, NR, K, S, BIG>,
-                                                     256, smem) != hipSuccess || occ < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, smem) != hipSuccess || occ < 1)
       occ = 1;
     (void)hipGetLastError();
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 16; ++i)
       if (occ_smem[i] == 0) {
         occ_smem[i] = smem;
         occ_val[i] = occ;
         break;
       }
   }
-  static const int persist = getenv("RV_CONV_PERSIST") ? atoi(getenv("RV_CONV_PERSIST")) : 1;
   const int T = (a.Cout + 15) / 16;
   const int ytiles = ceil_div(T, MR);
   const int ntiles = a.B * g.tiles_x * g.tiles_y;
   int gx = ntiles;
   if (persist) gx = std::min(ntiles, std::max(1, num_cus() * occ / ytiles));
   dim3 grid(gx, ytiles);
-  conv_patch_kernel<MR, NR, K, S, BIG><<<grid, 256, smem, s>>>(a, g);
+  fn<<<grid, 256, smem, s>>>(a, g);
   return launch_status("conv_patch");
-}
-
-template <int MR, int NR, int K, int S>
-static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, hipStream_t s) {
-  if (smem > 64 * 1024) return launch_patch_tb<MR, NR, K, S, true>(a, g, smem, s);
-  return launch_patch_tb<MR, NR, K, S, false>(a, g, smem, s);
 }
 
 // stride-2 patches are ~4x the tile: only tiles whose offset registers and
@@ -656,79 +698,144 @@ constexpr bool patch_s2_ok() {
   return NR <= 2 && MR * NR <= 8;
 }
 
-template <int MR, int NR>
-static int launch_patch_ks(const ConvArgs& a, const PatchGeo& g, size_t smem, hipStream_t s) {
-  if (a.k == 3 && a.stride == 1) return launch_patch_t<MR, NR, 3, 1>(a, g, smem, s);
-  if (a.k == 1 && a.stride == 1) return launch_patch_t<MR, NR, 1, 1>(a, g, smem, s);
-  if constexpr (patch_s2_ok<MR, NR>()) {
-    if (a.k == 3) return launch_patch_t<MR, NR, 3, 2>(a, g, smem, s);
-    return launch_patch_t<MR, NR, 1, 2>(a, g, smem, s);
+// Staged-weight (non-RESW) 3x3 variants with the biggest tiles exceed the
+// register file (scratch spills); they are not built.
+constexpr bool patch_spills(int MR, int NR, int K, int S, bool RESW) {
+  return !RESW && K == 3 && (MR * NR >= 16 || (S == 2 && MR * NR >= 8));
+}
+
+template <int MR, int NR, bool RESW>
+static int launch_patch_ks(const ConvArgs& a, const PatchGeo& g, size_t smem, int persist,
+                           hipStream_t s) {
+  if constexpr (!patch_spills(MR, NR, 3, 1, RESW))
+    if (a.k == 3 && a.stride == 1) return launch_patch_t<MR, NR, 3, 1, RESW>(a, g, smem, persist, s);
+  if (a.k == 1 && a.stride == 1) return launch_patch_t<MR, NR, 1, 1, RESW>(a, g, smem, persist, s);
+  if constexpr (patch_s2_ok<MR, NR>() && !patch_spills(MR, NR, 3, 2, RESW)) {
+    if (a.k == 3 && a.stride == 2) return launch_patch_t<MR, NR, 3, 2, RESW>(a, g, smem, persist, s);
   }
-  set_error("conv_patch: no stride-2 variant MR=%d NR=%d", MR, NR);
+  set_error("conv_patch: no variant MR=%d NR=%d k=%d s=%d", MR, NR, a.k, a.stride);
   return RV_EINVAL;
 }
 
-// returns 1 if launched (status in *st), 0 if the patch kernel does not apply
-static int try_launch_patch(const ConvArgs& a_in, hipStream_t s, int* st) {
-  ConvArgs a = a_in;
-  static const char* force = getenv("RV_CONV_FORCE");  // "direct" or "MR,NR" (experiments)
+// (MR, NR) tiles built for the patch kernel
+static const int kTiles[][2] = {{8, 2}, {8, 1}, {5, 2}, {5, 1}, {4, 4}, {4, 2}, {4, 1},
+                                {2, 4}, {2, 2}, {2, 1}, {1, 4}, {1, 2}, {1, 1}};
+
+bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c) {
   const int T = (a.Cout + 15) / 16;
-  if (force && strcmp(force, "direct") == 0) return 0;
-  struct Cand {
-    int mr, nr;
-  };
-  static const Cand cands[] = {{4, 4}, {8, 2}, {4, 2}, {2, 4}, {8, 1}, {4, 1}, {2, 2}, {1, 4},
-                               {2, 1}, {1, 2}, {1, 1}};
-  // Largest wave tile that still fills the machine: blocks >= 3/4 of the
-  // CUs x co-resident blocks per CU (LDS-limited, at most 4); otherwise the
-  // candidate with the best fill.
-  int best = -1;
-  double best_fill = -1.0;
-  PatchGeo bg{};
-  size_t bsm = 0;
-  for (int i = 0; i < (int)(sizeof(cands) / sizeof(cands[0])); ++i) {
-    const Cand& c = cands[i];
-    if (c.mr > T && c.mr > 1) continue;
-    if (ceil_div(T, c.mr) * c.mr - T > (c.mr > 1 ? 1 : 0)) continue;
-    if (a.k == 3 && c.mr > 4) continue;  // keep 3x3 weight stages <= 37 KB
-    if (a.stride == 2 && (c.nr > 2 || c.mr * c.nr > 8)) continue;  // patch_s2_ok
-    PatchGeo g;
-    size_t sm;
-    if (!patch_geo(a, c.nr, c.mr, g, sm)) continue;
-    if (force) {
-      int fm = 0, fn = 0;
-      if (sscanf(force, "%d,%d", &fm, &fn) == 2 && (fm != c.mr || fn != c.nr)) continue;
+  if (c.mr > T && c.mr > 1) return false;
+  if (a.stride == 2 && (c.nr > 2 || c.mr * c.nr > 8 || a.k != 3)) return false;  // patch_s2_ok
+  if (a.g2_cout0 > 0 && a.g2_cout0 % (16 * c.mr) != 0) return false;  // tiles inside one group
+  if (patch_spills(c.mr, c.nr, a.k, a.stride, c.resw != 0)) return false;
+  PatchGeo g;
+  size_t sm;
+  return patch_geo(a, c, g, sm);
+}
+
+int launch_conv_cfg(const ConvArgs& a, const ConvCfg& c, hipStream_t s) {
+  PatchGeo g;
+  size_t sm;
+  if (!conv_cfg_ok(a, c) || !patch_geo(a, c, g, sm)) {
+    set_error("conv config MR=%d NR=%d G=%d resw=%d not valid for this layer", c.mr, c.nr, c.G,
+              c.resw);
+    return RV_EINVAL;
+  }
+#define RV_PATCH(M_, N_)                                                                     \
+  if (c.mr == M_ && c.nr == N_)                                                              \
+    return c.resw ? launch_patch_ks<M_, N_, true>(a, g, sm, c.persist, s)                    \
+                  : launch_patch_ks<M_, N_, false>(a, g, sm, c.persist, s);
+  RV_PATCH(8, 2) RV_PATCH(8, 1) RV_PATCH(5, 2) RV_PATCH(5, 1) RV_PATCH(4, 4) RV_PATCH(4, 2)
+  RV_PATCH(4, 1) RV_PATCH(2, 4) RV_PATCH(2, 2) RV_PATCH(2, 1) RV_PATCH(1, 4) RV_PATCH(1, 2)
+  RV_PATCH(1, 1)
+#undef RV_PATCH
+  set_error("no conv_patch tile MR=%d NR=%d", c.mr, c.nr);
+  return RV_EINVAL;
+}
+
+// Every valid configuration of this layer (the autotuner's search space):
+// each tile with resident weights (largest G that fits) and with staged
+// weights (the largest G that fits, and G = 1); persistent grid.
+int conv_candidates(const ConvArgs& a, ConvCfg* out, int cap) {
+  int n = 0;
+  const int nch = conv_nch(a);
+  for (const auto& t : kTiles) {
+    for (int resw = 1; resw >= 0; --resw) {
+      int gbest = 0;
+      for (int G = nch; G >= 1 && !gbest; --G)
+        if (conv_cfg_ok(a, ConvCfg{t[0], t[1], G, resw, 1})) gbest = G;
+      if (!gbest) continue;
+      if (n < cap) out[n] = ConvCfg{t[0], t[1], gbest, resw, 1};
+      ++n;
+      if (!resw && gbest > 1) {
+        if (n < cap) out[n] = ConvCfg{t[0], t[1], 1, resw, 1};
+        ++n;
+      }
     }
-    const long blocks = (long)a.B * g.tiles_x * g.tiles_y * ceil_div(T, c.mr);
+  }
+  return n;
+}
+
+// Default (untuned) choice: the largest wave tile that still fills the
+// machine (blocks >= 3/4 of CUs x co-resident blocks), resident weights and
+// the largest chunk group that fit.
+static bool default_cfg(const ConvArgs& a, ConvCfg& best) {
+  const int T = (a.Cout + 15) / 16;
+  double best_fill = -1.0;
+  bool found = false;
+  for (const auto& t : kTiles) {
+    if (ceil_div(T, t[0]) * t[0] - T > (t[0] > 1 ? 1 : 0)) continue;
+    if (a.k == 3 && t[0] > 5) continue;  // keep 3x3 weight stages modest
+    ConvCfg cand{0, 0, 0, 0, 1};
+    bool ok = false;
+    for (int resw = 1; resw >= 0 && !ok; --resw)
+      for (int G = conv_nch(a); G >= 1 && !ok; --G) {
+        cand = ConvCfg{t[0], t[1], G, resw, 1};
+        ok = conv_cfg_ok(a, cand);
+      }
+    if (!ok) continue;
+    PatchGeo g;
+    size_t sm = 0;
+    patch_geo(a, cand, g, sm);
+    const long blocks = (long)a.B * g.tiles_x * g.tiles_y * ceil_div(T, t[0]);
     const int bpc = std::max(1, std::min(4, (int)((160 * 1024) / sm)));
     const double fill = (double)blocks / (256.0 * bpc);
     if (fill >= 0.75) {
-      best = i;
-      bg = g;
-      bsm = sm;
-      break;
+      best = cand;
+      return true;
     }
     if (fill > best_fill) {
       best_fill = fill;
-      best = i;
-      bg = g;
-      bsm = sm;
+      best = cand;
+      found = true;
     }
   }
-  if (best < 0) return 0;
-  const int MR = cands[best].mr, NR = cands[best].nr;
-  static const int dbg = getenv("RV_CONV_DEBUG") ? atoi(getenv("RV_CONV_DEBUG")) : 0;
-  if (dbg) {
-    const long blocks = (long)a.B * bg.tiles_x * bg.tiles_y * ceil_div(T, MR);
-    fprintf(stderr, "[conv] %dx%d k%d s%d Cin %d Cout %d -> patch MR=%d NR=%d tile %dx%d patch %dx%d smem %zu blocks %ld\n",
-            a.Ho, a.Wo, a.k, a.stride, a.Cin, a.Cout, MR, NR, bg.R, bg.C, bg.PH, bg.PW, bsm, blocks);
+  return found;
+}
+
+// returns 1 if launched (status in *st), 0 if the patch kernel does not apply
+static int try_launch_patch(const ConvArgs& a, hipStream_t s, int* st) {
+  static const char* force = getenv("RV_CONV_FORCE");  // "direct" or "MR,NR[,G,resw]"
+  if (force && strcmp(force, "direct") == 0) return 0;
+  ConvCfg c{0, 0, 1, 0, 1};
+  if (force) {
+    int fm = 0, fn = 0, fg = 1, fr = 0;
+    if (sscanf(force, "%d,%d,%d,%d", &fm, &fn, &fg, &fr) >= 2) {
+      c = ConvCfg{fm, fn, fg, fr, 1};
+      if (conv_cfg_ok(a, c)) {
+        *st = launch_conv_cfg(a, c, s);
+        return 1;
+      }
+    }
   }
-#define RV_PATCH(mr, nr) \
-  if (MR == mr && NR == nr) { *st = launch_patch_ks<mr, nr>(a, bg, bsm, s); return 1; }
-  RV_PATCH(4, 4) RV_PATCH(8, 2) RV_PATCH(4, 2) RV_PATCH(2, 4) RV_PATCH(8, 1) RV_PATCH(4, 1)
-  RV_PATCH(2, 2) RV_PATCH(1, 4) RV_PATCH(2, 1) RV_PATCH(1, 2) RV_PATCH(1, 1)
-#undef RV_PATCH
-  return 0;
+  if (!default_cfg(a, c)) return 0;
+  static const int persist = getenv("RV_CONV_PERSIST") ? atoi(getenv("RV_CONV_PERSIST")) : 1;
+  c.persist = persist;
+  static const int dbg = getenv("RV_CONV_DEBUG") ? atoi(getenv("RV_CONV_DEBUG")) : 0;
+  if (dbg)
+    fprintf(stderr, "[conv] %dx%d k%d s%d Cin %d Cout %d -> MR=%d NR=%d G=%d resw=%d\n", a.Ho, a.Wo,
+            a.k, a.stride, a.Cin, a.Cout, c.mr, c.nr, c.G, c.resw);
+  *st = launch_conv_cfg(a, c, s);
+  return 1;
 }
 
 // ---------------------------------------------------------------------------

@@ -8,6 +8,8 @@
 // the launch sequence of a forward.  Concats are free (producers write into
 // channel slices of the concat buffers); nearest-2x upsamples are extra
 // epilogue writes of the producing conv.
+#include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <vector>
 #include <cstring>
@@ -189,7 +191,9 @@ struct Profile {
 struct Model {
   ModelDef def;
   Profile prof;
-  std::vector<TraceRec> trace;  // conv launches of the last forward
+  std::vector<TraceRec> trace;  // conv specs run by the last forward (one record each)
+  std::vector<ConvArgs> launches;  // conv kernel launches of the last forward
+  std::vector<ConvCfg> tuned;      // per launch index: autotuned config (mr 0 = default)
   std::vector<std::pair<std::string, int>> tmps;  // bottleneck temp buffer per "prefix.m.i"
   int tmp_of(const std::string& k) const {
     for (auto& t : tmps)
@@ -289,17 +293,17 @@ struct Exec {
   const bf16_t* wptr(const ConvSpec& c) const { return (const bf16_t*)(M->dev + c.w_off); }
   const float* bptr(const ConvSpec& c) const { return (const float*)(M->dev + c.b_off); }
 
-  // conv `name`: input view at map level li -> up to two output views
-  void conv(const std::string& name, View in, int li, View o0, int up0 = 0, View o1 = {-1, 0, 0},
-            int up1 = 0, View res = {-1, 0, 0}) {
-    if (status) return;
+  int spec(const std::string& name) {
     const int idx = M->def.find(name);
-    if (idx < 0) {
+    if (idx < 0 && !status) {
       set_error("plan: unknown conv %s", name.c_str());
       status = RV_EINVAL;
-      return;
     }
-    const ConvSpec& c = M->def.convs[idx];
+    return idx;
+  }
+
+  ConvArgs args(const ConvSpec& c, View in, int li, View o0, int up0, View o1, int up1,
+                View res) const {
     ConvArgs a;
     memset(&a, 0, sizeof(a));
     a.in = (const bf16_t*)ptr(in.buf);
@@ -334,6 +338,11 @@ struct Exec {
       a.res_co = res.co;
     }
     a.act = c.act;
+    return a;
+  }
+
+  // one record per conv spec (layer-wise parity tests read these back)
+  void trace(int idx, const ConvArgs& a, View in, View o0, int up0, View o1, int up1, View res) {
     TraceRec r;
     memset(&r, 0, sizeof(r));
     r.conv = idx;
@@ -355,17 +364,77 @@ struct Exec {
     r.res_buf = res.buf;
     r.res_cs = res.cs;
     r.res_co = res.co;
-    const int li_ = (int)M->trace.size();
     M->trace.push_back(r);
+  }
+
+  static double flops_of(const ConvSpec& c, const ConvArgs& a) {
+    return 2.0 * a.B * a.Ho * a.Wo * (double)c.cout * c.cin * c.k * c.k;
+  }
+
+  // One kernel launch: the autotuned configuration of this launch index if
+  // there is a valid one, else the default; live HIP-event timing when
+  // profiling is on.
+  void launch(const ConvArgs& a, int idx, double flops) {
+    const int li_ = (int)M->launches.size();
+    M->launches.push_back(a);
     Profile& P = M->prof;
     const bool rec = P.on && P.n_fwd < P.cap_fwd && li_ < P.per_fwd;
     if (rec) hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + li_) * 2], s);
-    status = launch_conv(a, s);
+    if (li_ < (int)M->tuned.size() && M->tuned[li_].mr > 0 && conv_cfg_ok(a, M->tuned[li_]))
+      status = launch_conv_cfg(a, M->tuned[li_], s);
+    else
+      status = launch_conv(a, s);
     if (rec) hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + li_) * 2 + 1], s);
     if (P.on && P.n_fwd == 0 && li_ < P.per_fwd) {
-      P.flops[li_] = 2.0 * B * a.Ho * a.Wo * (double)c.cout * c.cin * c.k * c.k;
+      P.flops[li_] = flops;
       P.conv_of[li_] = idx;
     }
+  }
+
+  // conv `name`: input view at map level li -> up to two output views
+  void conv(const std::string& name, View in, int li, View o0, int up0 = 0, View o1 = {-1, 0, 0},
+            int up1 = 0, View res = {-1, 0, 0}) {
+    if (status) return;
+    const int idx = spec(name);
+    if (idx < 0) return;
+    const ConvSpec& c = M->def.convs[idx];
+    const ConvArgs a = args(c, in, li, o0, up0, o1, up1, res);
+    trace(idx, a, in, o0, up0, o1, up1, res);
+    launch(a, idx, flops_of(c, a));
+  }
+
+  // Two convs that share their input buffer, kernel size, stride and
+  // activation and write adjacent channel slices of one output view -- the
+  // Detect head's cv2 / cv3 branches -- as one grouped launch
+  // (ConvArgs::g2_*).  RV_HEAD_PAIR=0 launches them separately.
+  void conv_pair(const std::string& n1, View in1, const std::string& n2, View in2, int li,
+                 View o0) {
+    if (status) return;
+    const int i1 = spec(n1), i2 = spec(n2);
+    if (i1 < 0 || i2 < 0) return;
+    const ConvSpec& c1 = M->def.convs[i1];
+    const ConvSpec& c2 = M->def.convs[i2];
+    const View o2{o0.buf, o0.cs, o0.co + c1.cout};
+    static const bool pair = !getenv("RV_HEAD_PAIR") || atoi(getenv("RV_HEAD_PAIR")) != 0;
+    if (!pair || in1.buf != in2.buf || in1.cs != in2.cs || c1.k != c2.k || c1.s != c2.s ||
+        c1.act != c2.act || c1.cout % 64 != 0) {
+      conv(n1, in1, li, o0);
+      conv(n2, in2, li, o2);
+      return;
+    }
+    const View none{-1, 0, 0};
+    ConvArgs a = args(c1, in1, li, o0, 0, none, 0, none);
+    const ConvArgs a2 = args(c2, in2, li, o2, 0, none, 0, none);
+    trace(i1, a, in1, o0, 0, none, 0, none);
+    trace(i2, a2, in2, o2, 0, none, 0, none);
+    const double fl = flops_of(c1, a) + flops_of(c2, a2);
+    a.Cout = c1.cout + c2.cout;
+    a.g2_cout0 = c1.cout;
+    a.g2_in_co = in2.co;
+    a.g2_Cin = c2.cin;
+    a.g2_w = wptr(c2);
+    a.g2_bias = bptr(c2);
+    launch(a, i1, fl);
   }
 
   // C2f(prefix): in view (map li) -> concat buffer cb -> outputs
@@ -521,6 +590,7 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
     off = (off + b.elems_per_img * B * (b.f32 ? 4 : 2) + 255) & ~(size_t)255;
   }
   M->trace.clear();
+  M->launches.clear();
   // backbone
   const ConvSpec& c0 = M->def.convs[0];
   int st = launch_conv0(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
@@ -561,14 +631,14 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   // Detect
   const View P[3] = {View{M->X15, v.h15, 0}, View{M->X18, v.h18, 0}, View{M->X21, v.h21, 0}};
   const int dcs = v.c2d + v.c3d, hcs = 4 * v.reg + v.nc;
+  // box (cv2) and class (cv3) branches of a level: one grouped launch per stage
   for (int i = 0; i < 3; ++i) {
     const std::string a = "model.22.cv2." + std::to_string(i), c = "model.22.cv3." + std::to_string(i);
-    E.conv(a + ".0", P[i], 3 + i, View{M->DA[i], dcs, 0});
-    E.conv(c + ".0", P[i], 3 + i, View{M->DA[i], dcs, v.c2d});
-    E.conv(a + ".1", View{M->DA[i], dcs, 0}, 3 + i, View{M->DB[i], dcs, 0});
-    E.conv(c + ".1", View{M->DA[i], dcs, v.c2d}, 3 + i, View{M->DB[i], dcs, v.c2d});
-    E.conv(a + ".2", View{M->DB[i], dcs, 0}, 3 + i, View{M->HD[i], hcs, 0});
-    E.conv(c + ".2", View{M->DB[i], dcs, v.c2d}, 3 + i, View{M->HD[i], hcs, 4 * v.reg});
+    E.conv_pair(a + ".0", P[i], c + ".0", P[i], 3 + i, View{M->DA[i], dcs, 0});
+    E.conv_pair(a + ".1", View{M->DA[i], dcs, 0}, c + ".1", View{M->DA[i], dcs, v.c2d}, 3 + i,
+                View{M->DB[i], dcs, 0});
+    E.conv_pair(a + ".2", View{M->DB[i], dcs, 0}, c + ".2", View{M->DB[i], dcs, v.c2d}, 3 + i,
+                View{M->HD[i], hcs, 0});
   }
   if (E.status) return E.status;
   if (M->prof.on && M->prof.n_fwd < M->prof.cap_fwd) M->prof.n_fwd++;
@@ -658,4 +728,140 @@ extern "C" int rv_yolo_profile_read(void* h, double* ms, double* flops, int* con
     conv[i] = P.conv_of[i];
   }
   return P.n_fwd;
+}
+
+// ---- per-layer autotuning ---------------------------------------------------
+namespace rv {
+
+// Bytes of the buffer an output view lives in (the view's base pointer is
+// the buffer start): B x (2x upsampled) rows x channel stride x element.
+static size_t out_bytes(const ConvArgs& a, int d) {
+  const void* p = d == 0 ? a.out0 : a.out1;
+  if (!p) return 0;
+  const int up = d == 0 ? a.out0_up : a.out1_up;
+  const int cs = d == 0 ? a.out0_cs : a.out1_cs;
+  return (size_t)a.B * a.Ho * a.Wo * (up ? 4 : 1) * cs * (a.out_f32 ? 4 : 2);
+}
+
+__global__ void count_diff_kernel(const uint32_t* __restrict__ x, const uint32_t* __restrict__ y,
+                                  size_t n, unsigned* __restrict__ cnt) {
+  unsigned c = 0;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    c += x[i] != y[i];
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
+}
+
+}  // namespace rv
+
+// Time every valid kernel configuration of every conv launch of a forward on
+// this input (the activations of one default forward, so every launch sees
+// its real operands) and keep the fastest per launch index for later
+// forwards of this handle.  Synchronous; not capturable.  verify != 0 also
+// compares each configuration's output buffers with the default's (all
+// configurations accumulate in the same k order, so they must be bit-equal);
+// *n_bad = configurations that differed.
+extern "C" int rv_yolo_autotune(void* h, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
+                                int reps, int verify, int* n_bad, void* stream) {
+  RV_CHECK_ARG(h && lb && ws, "null pointer");
+  Model* M = (Model*)h;
+  hipStream_t s = as_stream(stream);
+  reps = reps < 1 ? 1 : reps;
+  M->tuned.clear();
+  int st = rv_yolo_forward(h, lb, B, ws, ws_bytes, nullptr, 1.0f, nullptr, 0, nullptr, stream);
+  if (st) return st;
+  const std::vector<ConvArgs> L = M->launches;
+  std::vector<ConvCfg> best(L.size(), ConvCfg{0, 0, 0, 0, 0});
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+    set_error("hipEventCreate failed");
+    return RV_EINVAL;
+  }
+  size_t maxb = 0;
+  for (const ConvArgs& a : L) maxb = std::max(maxb, std::max(out_bytes(a, 0), out_bytes(a, 1)));
+  uint8_t* ref = nullptr;
+  unsigned* cnt = nullptr;
+  if (verify && (hipMalloc((void**)&ref, 2 * maxb) != hipSuccess ||
+                 hipMalloc((void**)&cnt, sizeof(unsigned)) != hipSuccess)) {
+    set_error("autotune: hipMalloc of %zu verification bytes failed", 2 * maxb);
+    st = RV_EINVAL;
+  }
+  int bad = 0;
+  static const int dbg = getenv("RV_CONV_DEBUG") ? atoi(getenv("RV_CONV_DEBUG")) : 0;
+  std::vector<ConvCfg> cands(256);
+  for (size_t i = 0; i < L.size() && !st; ++i) {
+    const ConvArgs& a = L[i];
+    if (verify)
+      for (int d = 0; d < 2; ++d)
+        if (out_bytes(a, d))
+          hipMemcpyAsync(ref + d * maxb, d == 0 ? a.out0 : a.out1, out_bytes(a, d),
+                         hipMemcpyDeviceToDevice, s);
+    auto time_cfg = [&](const ConvCfg* c) -> float {
+      int r = c ? launch_conv_cfg(a, *c, s) : launch_conv(a, s);  // warm-up launch
+      hipEventRecord(e0, s);
+      for (int k = 0; k < reps && !r; ++k) r = c ? launch_conv_cfg(a, *c, s) : launch_conv(a, s);
+      hipEventRecord(e1, s);
+      if (r || hipEventSynchronize(e1) != hipSuccess) {
+        if (!st) st = r ? r : RV_EINVAL;
+        return 1e30f;
+      }
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, e0, e1);
+      return ms / reps;
+    };
+    const float t0 = time_cfg(nullptr);
+    float tbest = t0;
+    const int n = std::min(conv_candidates(a, cands.data(), (int)cands.size()), (int)cands.size());
+    for (int j = 0; j < n && !st; ++j) {
+      const float t = time_cfg(&cands[j]);
+      if (verify) {
+        unsigned diff = 0;
+        for (int d = 0; d < 2; ++d) {
+          const size_t nb = out_bytes(a, d);
+          if (!nb) continue;
+          hipMemsetAsync(cnt, 0, sizeof(unsigned), s);
+          count_diff_kernel<<<1024, 256, 0, s>>>((const uint32_t*)(ref + d * maxb),
+                                                 (const uint32_t*)(d == 0 ? a.out0 : a.out1),
+                                                 nb / 4, cnt);
+          unsigned h_cnt = 0;
+          hipMemcpyAsync(&h_cnt, cnt, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+          hipStreamSynchronize(s);
+          diff += h_cnt;
+        }
+        if (diff) ++bad;
+      }
+      if (t < tbest) {
+        tbest = t;
+        best[i] = cands[j];
+      }
+    }
+    if (dbg)
+      fprintf(stderr, "[autotune] launch %2zu %3dx%-3d k%d s%d %4d->%-4d default %7.1f us best %7.1f us"
+                      " MR=%d NR=%d G=%d resw=%d (%d cfgs)\n",
+              i, a.Ho, a.Wo, a.k, a.stride, a.Cin, a.Cout, t0 * 1e3, tbest * 1e3, best[i].mr,
+              best[i].nr, best[i].G, best[i].resw, n);
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (ref) hipFree(ref);
+  if (cnt) hipFree(cnt);
+  if (n_bad) *n_bad = bad;
+  if (!st) M->tuned = best;
+  return st;
+}
+
+// The autotuned configuration of conv launch `idx` (cfg5 = {MR, NR, G, resw,
+// persist}; MR = 0: the default heuristic).  Returns the number of launches.
+extern "C" int rv_yolo_tuned_config(void* h, int idx, int* cfg5) {
+  if (!h) return RV_EINVAL;
+  Model* M = (Model*)h;
+  if (cfg5 && idx >= 0 && idx < (int)M->tuned.size()) {
+    const ConvCfg& c = M->tuned[idx];
+    cfg5[0] = c.mr;
+    cfg5[1] = c.nr;
+    cfg5[2] = c.G;
+    cfg5[3] = c.resw;
+    cfg5[4] = c.persist;
+  }
+  return (int)M->tuned.size();
 }

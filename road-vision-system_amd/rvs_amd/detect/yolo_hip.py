@@ -121,6 +121,29 @@ class YoloEngine:
         self._nseg_cur = self.nseg
         return raw
 
+    def autotune(self, lb: torch.Tensor, reps: int = 3, verify: bool = False) -> int:
+        """Pick the fastest kernel configuration of every conv launch on this
+        letterboxed batch (rv_yolo_autotune; synchronous, not capturable).
+        Returns the number of configurations whose output differed from the
+        default's (verify=True; 0 expected: all are bit-identical)."""
+        B = lb.shape[0]
+        lb = lb.contiguous()
+        bad = ctypes.c_int(0)
+        call("rv_yolo_autotune", self._h, ptr(lb), B, ptr(self.ws), self.ws_bytes, int(reps),
+             1 if verify else 0, ctypes.byref(bad), stream_ptr())
+        return bad.value
+
+    def tuned_configs(self):
+        """[(MR, NR, G, resw, persist)] per conv launch ([] before autotune)."""
+        lib = _lib.load()
+        n = lib.rv_yolo_tuned_config(self._h, -1, None)
+        out = []
+        for i in range(max(n, 0)):
+            c = (ctypes.c_int * 5)()
+            lib.rv_yolo_tuned_config(self._h, i, c)
+            out.append(tuple(c))
+        return out
+
     def nms(self, B: int, slot: int = 0):
         """NMS + scale_boxes + class filter of candidate slot `slot`."""
         call("rv_nms_postprocess", ptr(self.cand[slot]), ptr(self.seg_n[slot]), B, self.cap,

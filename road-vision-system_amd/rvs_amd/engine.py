@@ -78,6 +78,12 @@ class RoadVisionEngine:
         self.yolo_stage(lb, slot)
         return proc
 
+    def autotune(self, frames: torch.Tensor, reps: int = 3, verify: bool = False) -> int:
+        """Autotune the detector's conv kernels on one batch of these frames
+        (YoloEngine.autotune); call outside graph capture."""
+        _, lb = self.preprocess_stage(frames)
+        return self.detector.autotune(lb, reps=reps, verify=verify)
+
     def track_stage(self, ts: torch.Tensor, slot: int = 0) -> Dict[str, torch.Tensor]:
         """NMS of candidate slot `slot` + SORT/geometry (main_preview.py:99-109)."""
         dets, det_n = self.detector.nms(ts.shape[0], slot)

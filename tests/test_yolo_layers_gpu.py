@@ -175,3 +175,26 @@ def test_first_conv_sppf_and_decode(cuda):
     n = int(eng.seg_n.view(-1)[:eng.nseg].sum())  # image 0's segments
     expect = int((raw[0, 4:].max(0) > 0.25).sum())
     assert n == expect
+
+
+def test_autotuned_configs_are_bit_identical(cuda):
+    """rv_yolo_autotune times every valid kernel configuration of every conv
+    launch (tile shape, chunk group, resident weights) and checks each
+    configuration's output buffers against the default's: all accumulate in
+    the same k order, so they must agree bit for bit.  The tuned forward must
+    then reproduce the default forward's raw prediction exactly."""
+    from rvs_amd.detect import weights
+    from rvs_amd.detect.yolo_hip import YoloEngine
+    H, W, B = 1080, 1920, 2
+    eng = YoloEngine(0, weights.synthetic_weights(0, seed=2), B, (H, W), device=cuda)
+    fr = np.stack([cpu.median(cpu.clahe_ycrcb(road_frame(H, W, seed=50 + b)), 3) for b in range(B)])
+    lb = eng.letterbox(torch.from_numpy(fr).to(cuda))
+    raw0 = torch.empty((B, 84, eng.A), dtype=torch.float32, device=cuda)
+    eng.forward_raw(lb, raw0)
+    assert eng.autotune(lb, reps=1, verify=True) == 0
+    cfgs = eng.tuned_configs()
+    assert len(cfgs) > 0 and all(c[0] >= 0 for c in cfgs)
+    raw1 = torch.empty_like(raw0)
+    eng.forward_raw(lb, raw1)
+    np.testing.assert_array_equal(raw1.cpu().numpy(), raw0.cpu().numpy())
+    eng.close()
