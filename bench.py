@@ -172,6 +172,12 @@ def main():
     n_launch = int(valid.sum())
     achieved = conv_flop_per_step / (conv_ms_per_step * 1e-3) / 1e12 if conv_ms_per_step else 0.0
 
+    # HBM bytes of the conv_patch launches of one step, from the committed
+    # PMC passes of this configuration (tools/gpu_pmc.sh -> pmc_traffic.json)
+    traffic = None
+    tp = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
+    if os.path.exists(tp):
+        traffic = json.load(open(tp)).get("conv_patch_bytes_per_step")
     total_frames = world * S * K
     value = total_frames / elapsed
     res = {
@@ -200,7 +206,8 @@ def main():
         "roofline": {
             "kernel": "conv_patch (all YOLOv8n conv launches of a step, HIP events)",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16,
-            "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 5), "traffic": None,
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 5), "traffic": traffic,
+            "traffic_unit": "bytes per step (all conv_patch launches; PMC, profiles/r01)",
             "launches_per_step": n_launch,
             "conv_ms_per_step": round(conv_ms_per_step, 4),
             "conv_gflop_per_step": round(conv_flop_per_step / 1e9, 2),

@@ -70,6 +70,17 @@ struct HeadLevel {
   const float* logits;  // [B][H][W][cs] f32: [0,4*reg) box bins, [4*reg, 4*reg+nc) classes
   int H, W, cs;
   float stride;
+  // fused form (feat != nullptr): the last 1x1 convs of the level run inside
+  // the decode from the bf16 features [box feats (cin_b) | class feats
+  // (cin_c)] (channel stride feat_cs) with packed weights [cout][cin_pad32]
+  // and f32 biases; logits_out (nullable) receives the f32 logits.
+  const bf16_t* feat;
+  int feat_cs, cin_b, cin_c;
+  const bf16_t* w_box;
+  const bf16_t* w_cls;
+  const float* b_box;
+  const float* b_cls;
+  float* logits_out;
 };
 
 struct Cand {  // one detection candidate (Ultralytics NMS row before NMS)

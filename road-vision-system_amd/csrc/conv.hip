@@ -754,7 +754,8 @@ int launch_conv_cfg(const ConvArgs& a, const ConvCfg& c, hipStream_t s) {
 
 // Every valid configuration of this layer (the autotuner's search space):
 // each tile with resident weights (largest G that fits) and with staged
-// weights (the largest G that fits, and G = 1); persistent grid.
+// weights (the largest G that fits, and G = 1); persistent grid or one
+// block per pixel tile.
 int conv_candidates(const ConvArgs& a, ConvCfg* out, int cap) {
   int n = 0;
   const int nch = conv_nch(a);
@@ -764,11 +765,14 @@ int conv_candidates(const ConvArgs& a, ConvCfg* out, int cap) {
       for (int G = nch; G >= 1 && !gbest; --G)
         if (conv_cfg_ok(a, ConvCfg{t[0], t[1], G, resw, 1})) gbest = G;
       if (!gbest) continue;
-      if (n < cap) out[n] = ConvCfg{t[0], t[1], gbest, resw, 1};
-      ++n;
-      if (!resw && gbest > 1) {
-        if (n < cap) out[n] = ConvCfg{t[0], t[1], 1, resw, 1};
+      // persistent grid, and (for layers with few tiles) one block per tile
+      for (int persist = 1; persist >= 0; --persist) {
+        if (n < cap) out[n] = ConvCfg{t[0], t[1], gbest, resw, persist};
         ++n;
+        if (!resw && gbest > 1) {
+          if (n < cap) out[n] = ConvCfg{t[0], t[1], 1, resw, persist};
+          ++n;
+        }
       }
     }
   }
@@ -1128,7 +1132,16 @@ struct HeadLevels {
 // part p takes the DFL side p (softmax expectation over REG bins) and the
 // classes p, p+4, ...; the quad then combines the four sides and the
 // first-max class with lane shuffles.
-template <int REG>
+//
+// FUSED: the head's last 1x1 convs (cv2.i.2: 4*REG box logits, cv3.i.2: nc
+// class logits, no activation) run here on MFMA from the level's bf16
+// features (L.feat, [box feats | class feats]) straight into the LDS logits
+// tile, so the f32 logits never touch HBM (L.logits, when non-null, still
+// receives them: the parity tests read it).  Wave w computes anchors
+// 16w..16w+15 of the block: box fragments m = 0..REG/4-1, class fragments
+// after them; B fragments are 16-B loads of one anchor's 8 channels, A
+// fragments 16-B loads of the packed [cout][cin_pad32] weights (L2-resident).
+template <int REG, bool FUSED>
 __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B, int nc,
                                                             float conf, float* __restrict__ raw,
                                                             Cand* __restrict__ cand, int cap,
@@ -1156,26 +1169,107 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
   const int na = min(64, HW - r0);
   const int tid = threadIdx.x;
   const int cs4 = L.cs / 4, ls4 = cs4 + 1;  // row length / LDS row stride in float4
-  const f32x4* src = (const f32x4*)(L.logits + ((size_t)b * HW + r0) * L.cs);
-  // 8 loads in flight per thread before any LDS store (a plain copy loop
-  // would wait out one HBM latency per element)
-  for (int i0 = tid; i0 < na * cs4; i0 += 8 * 256) {
-    f32x4 v[8];  // native vectors (a float4 struct array would live in scratch)
+  if constexpr (FUSED) {
+    constexpr int MB = REG / 4;  // box fragments (4*REG couts)
+    const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
+    const int an0 = wave * 16 + col;  // this lane's anchor (B column / D column)
+    const bool ok = an0 < na;
+    const bf16_t* fp = L.feat + ((size_t)b * HW + r0 + (ok ? an0 : 0)) * L.feat_cs + quad * 8;
+    const int ncf = (nc + 15) / 16;  // class fragments
+    float* lrow = lg + (size_t)an0 * (L.cs + 4);
+    // box: K = cin_b (multiple of 32)
+    {
+      f32x4 acc[MB];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * 256;
-      v[u] = i < na * cs4 ? src[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+      for (int m = 0; m < MB; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int cinp = (L.cin_b + 31) & ~31;
+      for (int k = 0; k < cinp; k += 32) {
+        const bool kv = ok && k + quad * 8 < L.cin_b;
+        const uint4 bv = kv ? *(const uint4*)(fp + k) : make_uint4(0, 0, 0, 0);
+        const bf16x8 Bf = __builtin_bit_cast(bf16x8, bv);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * 256;
-      if (i < na * cs4) {
-        const int row = i / cs4, c4 = i - (i / cs4) * cs4;
-        ((f32x4*)lg)[row * ls4 + c4] = v[u];
+        for (int m = 0; m < MB; ++m) {
+          const bf16x8 Af = __builtin_bit_cast(
+              bf16x8, *(const uint4*)(L.w_box + (size_t)(m * 16 + col) * cinp + k + quad * 8));
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af, Bf, acc[m], 0, 0, 0);
+        }
+      }
+      // lane holds couts m*16 + quad*4 + i of anchor `col` of this wave
+#pragma unroll
+      for (int m = 0; m < MB; ++m) {
+        const int co = m * 16 + quad * 4;
+        const f32x4 bb = *(const f32x4*)(L.b_box + co);
+        *(f32x4*)(lg + (size_t)(wave * 16 + col) * (L.cs + 4) + co) = acc[m] + bb;
       }
     }
+    // classes: K = cin_c, couts nc (padded to 16)
+    {
+      const int cinp = (L.cin_c + 31) & ~31;
+      for (int m0 = 0; m0 < ncf; m0 += 5) {  // up to 5 fragments (80 classes) per pass
+        f32x4 acc[5];
+#pragma unroll
+        for (int m = 0; m < 5; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < cinp; k += 32) {
+          const bool kv = ok && k + quad * 8 < L.cin_c;
+          const uint4 bv = kv ? *(const uint4*)(fp + 4 * REG + k) : make_uint4(0, 0, 0, 0);
+          const bf16x8 Bf = __builtin_bit_cast(bf16x8, bv);
+#pragma unroll
+          for (int m = 0; m < 5; ++m) {
+            if (m0 + m >= ncf) break;
+            const bf16x8 Af = __builtin_bit_cast(
+                bf16x8,
+                *(const uint4*)(L.w_cls + (size_t)((m0 + m) * 16 + col) * cinp + k + quad * 8));
+            acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af, Bf, acc[m], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < 5; ++m) {
+          if (m0 + m >= ncf) break;
+          const int co = (m0 + m) * 16 + quad * 4;  // class index (bias padded to 16)
+          const f32x4 bb = *(const f32x4*)(L.b_cls + co);
+          float* d = lg + (size_t)(wave * 16 + col) * (L.cs + 4) + 4 * REG + co;
+          const f32x4 v = acc[m] + bb;
+          // the last fragment may run past nc: keep the padding out of the row
+          if (co + 3 < nc) {
+            *(f32x4*)d = v;
+          } else {
+            for (int i = 0; i < 4; ++i)
+              if (co + i < nc) d[i] = v[i];
+          }
+        }
+      }
+    }
+    (void)lrow;
+    __syncthreads();
+    if (L.logits_out) {  // parity/debug copy of the logits (coalesced rows)
+      f32x4* dst = (f32x4*)(L.logits_out + ((size_t)b * HW + r0) * L.cs);
+      for (int i = tid; i < na * cs4; i += 256) {
+        const int row = i / cs4, c4 = i - (i / cs4) * cs4;
+        dst[i] = ((const f32x4*)lg)[row * ls4 + c4];
+      }
+    }
+  } else {
+    const f32x4* src = (const f32x4*)(L.logits + ((size_t)b * HW + r0) * L.cs);
+    // 8 loads in flight per thread before any LDS store (a plain copy loop
+    // would wait out one HBM latency per element)
+    for (int i0 = tid; i0 < na * cs4; i0 += 8 * 256) {
+      f32x4 v[8];  // native vectors (a float4 struct array would live in scratch)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 256;
+        v[u] = i < na * cs4 ? src[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 256;
+        if (i < na * cs4) {
+          const int row = i / cs4, c4 = i - (i / cs4) * cs4;
+          ((f32x4*)lg)[row * ls4 + c4] = v[u];
+        }
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const int an = tid >> 2, part = tid & 3;
   const bool live = an < na;
   const float* px = lg + (live ? an : 0) * (L.cs + 4);
@@ -1297,19 +1391,31 @@ int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_ma
     }
   }
   const size_t smem = (size_t)64 * (cs + 4) * 4;
-  static bool attr = false;
-  if (!attr && smem > 64 * 1024) {  // only raise the cap when the head needs it
-    hipFuncSetAttribute((const void*)detect_decode_kernel<16>,
+  const bool fused = lv[0].feat != nullptr;
+  static bool attr[2] = {false, false};
+  if (!attr[fused] && smem > 64 * 1024) {  // only raise the cap when the head needs it
+    hipFuncSetAttribute(fused ? (const void*)detect_decode_kernel<16, true>
+                              : (const void*)detect_decode_kernel<16, false>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();
-    attr = true;
+    attr[fused] = true;
   }
   if (cand && cand_cap < h.blk[nlv] * 64) {
     set_error("detect decode: cand_cap %d < %d segments x 64", cand_cap, h.blk[nlv]);
     return RV_EINVAL;
   }
-  detect_decode_kernel<16><<<dim3(h.blk[nlv], B), 256, smem, s>>>(h, B, nc, conf, raw, cand,
-                                                                  cand_cap, cand_n);
+  if (fused) {
+    for (int i = 0; i < nlv; ++i)
+      if (lv[i].cs != 4 * reg_max + nc || lv[i].cin_b % 8 || lv[i].cin_c % 8 || lv[i].feat_cs % 8) {
+        set_error("fused head: bad level %d geometry", i);
+        return RV_EINVAL;
+      }
+    detect_decode_kernel<16, true><<<dim3(h.blk[nlv], B), 256, smem, s>>>(h, B, nc, conf, raw, cand,
+                                                                          cand_cap, cand_n);
+  } else {
+    detect_decode_kernel<16, false><<<dim3(h.blk[nlv], B), 256, smem, s>>>(h, B, nc, conf, raw,
+                                                                           cand, cand_cap, cand_n);
+  }
   return launch_status("detect_decode");
 }
 

@@ -631,24 +631,55 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   // Detect
   const View P[3] = {View{M->X15, v.h15, 0}, View{M->X18, v.h18, 0}, View{M->X21, v.h21, 0}};
   const int dcs = v.c2d + v.c3d, hcs = 4 * v.reg + v.nc;
-  // box (cv2) and class (cv3) branches of a level: one grouped launch per stage
+  // box (cv2) and class (cv3) branches of a level: one grouped launch per
+  // stage; the last 1x1 stage runs inside the decode kernel (RV_FUSE_HEAD=0:
+  // separate launches and f32 logits in HBM)
+  static const bool fuse_env = !getenv("RV_FUSE_HEAD") || atoi(getenv("RV_FUSE_HEAD")) != 0;
+  const bool fuse_head = fuse_env && v.c2d % 8 == 0 && v.c3d % 8 == 0;
   for (int i = 0; i < 3; ++i) {
     const std::string a = "model.22.cv2." + std::to_string(i), c = "model.22.cv3." + std::to_string(i);
     E.conv_pair(a + ".0", P[i], c + ".0", P[i], 3 + i, View{M->DA[i], dcs, 0});
     E.conv_pair(a + ".1", View{M->DA[i], dcs, 0}, c + ".1", View{M->DA[i], dcs, v.c2d}, 3 + i,
                 View{M->DB[i], dcs, 0});
-    E.conv_pair(a + ".2", View{M->DB[i], dcs, 0}, c + ".2", View{M->DB[i], dcs, v.c2d}, 3 + i,
-                View{M->HD[i], hcs, 0});
+    if (!fuse_head) {
+      E.conv_pair(a + ".2", View{M->DB[i], dcs, 0}, c + ".2", View{M->DB[i], dcs, v.c2d}, 3 + i,
+                  View{M->HD[i], hcs, 0});
+    } else {  // run inside the decode kernel; trace records keep the layer list complete
+      const View none{-1, 0, 0};
+      const int ia = E.spec(a + ".2"), ic = E.spec(c + ".2");
+      if (ia < 0 || ic < 0) return E.status;
+      const ConvSpec& sa = M->def.convs[ia];
+      const ConvSpec& sc = M->def.convs[ic];
+      E.trace(ia, E.args(sa, View{M->DB[i], dcs, 0}, 3 + i, View{M->HD[i], hcs, 0}, 0, none, 0, none),
+              View{M->DB[i], dcs, 0}, View{M->HD[i], hcs, 0}, 0, none, 0, none);
+      E.trace(ic, E.args(sc, View{M->DB[i], dcs, v.c2d}, 3 + i, View{M->HD[i], hcs, 4 * v.reg}, 0,
+                         none, 0, none),
+              View{M->DB[i], dcs, v.c2d}, View{M->HD[i], hcs, 4 * v.reg}, 0, none, 0, none);
+    }
   }
   if (E.status) return E.status;
   if (M->prof.on && M->prof.n_fwd < M->prof.cap_fwd) M->prof.n_fwd++;
   HeadLevel hl[3];
+  memset(hl, 0, sizeof(hl));
   for (int i = 0; i < 3; ++i) {
     hl[i].logits = (const float*)E.ptr(M->HD[i]);
     hl[i].H = M->map_h[3 + i];
     hl[i].W = M->map_w[3 + i];
     hl[i].cs = hcs;
     hl[i].stride = (float)(8 << i);
+    if (fuse_head) {
+      const ConvSpec& sa = M->def.convs[M->def.find("model.22.cv2." + std::to_string(i) + ".2")];
+      const ConvSpec& sc = M->def.convs[M->def.find("model.22.cv3." + std::to_string(i) + ".2")];
+      hl[i].feat = (const bf16_t*)E.ptr(M->DB[i]);
+      hl[i].feat_cs = dcs;
+      hl[i].cin_b = sa.cin;
+      hl[i].cin_c = sc.cin;
+      hl[i].w_box = E.wptr(sa);
+      hl[i].w_cls = E.wptr(sc);
+      hl[i].b_box = E.bptr(sa);
+      hl[i].b_cls = E.bptr(sc);
+      hl[i].logits_out = raw_out ? (float*)E.ptr(M->HD[i]) : nullptr;
+    }
   }
   return launch_detect_decode(hl, 3, B, v.nc, v.reg, conf, raw_out, (Cand*)cand, cand_cap, cand_n,
                               E.s);
@@ -788,7 +819,7 @@ extern "C" int rv_yolo_autotune(void* h, const uint8_t* lb, int B, void* ws, siz
   }
   int bad = 0;
   static const int dbg = getenv("RV_CONV_DEBUG") ? atoi(getenv("RV_CONV_DEBUG")) : 0;
-  std::vector<ConvCfg> cands(256);
+  std::vector<ConvCfg> cands(512);
   for (size_t i = 0; i < L.size() && !st; ++i) {
     const ConvArgs& a = L[i];
     if (verify)

@@ -1,0 +1,46 @@
+"""HBM traffic of the conv_patch launches of one bench step from the PMC
+passes of tools/gpu_pmc.sh (FETCH_SIZE / WRITE_SIZE, KB): per the gfx950
+calibration in MI355X_MICROARCH.md, FETCH_SIZE counts half the bytes of a
+wide streaming read (x2), WRITE_SIZE counts 16-B-per-lane stores exactly.
+Writes a JSON file that bench.py reports as roofline.traffic.
+Usage: pmc_traffic.py out.json pass1.csv pass2.csv ..."""
+import json
+import os
+import sys
+
+sys.path[:0] = [os.path.dirname(os.path.abspath(__file__))]
+from pmc_report import load  # noqa: E402
+
+
+def main():
+    out = sys.argv[1]
+    passes = [load(p) for p in sys.argv[2:]]
+    n = min(len(p) for p in passes)
+    fetch = write = 0.0
+    per_kernel = {}
+    for i in range(n):
+        v = {}
+        for p in passes:
+            v.update({k: x for k, x in p[i].items() if k != "name"})
+        name = passes[0][i]["name"].split("(")[0].replace("void rv::", "").replace("rv::", "")
+        rd = 2 * v.get("FETCH_SIZE", 0.0) * 1024
+        wr = v.get("WRITE_SIZE", 0.0) * 1024
+        k = per_kernel.setdefault(name.split("<")[0], [0, 0.0, 0.0])
+        k[0] += 1
+        k[1] += rd
+        k[2] += wr
+        if name.startswith("conv_patch_kernel"):
+            fetch += rd
+            write += wr
+    res = {"conv_patch_bytes_per_step": fetch + write, "conv_patch_read_bytes": fetch,
+           "conv_patch_write_bytes": write,
+           "per_kernel": {k: {"launches": c, "read_bytes": r, "write_bytes": w}
+                          for k, (c, r, w) in per_kernel.items()},
+           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over one eager bench step "
+                     "(tools/gpu_pmc.sh); read = 2 x FETCH_SIZE (gfx950 calibration), KB -> B"}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "per_kernel"}))
+
+
+if __name__ == "__main__":
+    main()
