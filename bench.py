@@ -165,12 +165,20 @@ def main():
     fl = np.zeros(n, np.float64)
     cv = np.zeros(n, np.int32)
     nf = lib.rv_yolo_profile_read(eng.detector._h, ms.ctypes.data, fl.ctypes.data, cv.ctypes.data, n)
+    by = np.zeros(n, np.float64)
+    lib.rv_yolo_profile_bytes(eng.detector._h, by.ctypes.data, n)
     lib.rv_yolo_profile(eng.detector._h, 0)
     valid = cv >= 0
     conv_ms_per_step = float(ms[valid].sum()) / max(nf, 1)
     conv_flop_per_step = float(fl[valid].sum())
+    conv_bytes_per_step = float(by[valid].sum())
     n_launch = int(valid.sum())
     achieved = conv_flop_per_step / (conv_ms_per_step * 1e-3) / 1e12 if conv_ms_per_step else 0.0
+    achieved_bw = conv_bytes_per_step / (conv_ms_per_step * 1e-3) / 1e9 if conv_ms_per_step else 0.0
+    # which roofline binds the conv family: its algorithmic bytes at peak HBM
+    # vs its FLOPs at peak bf16 MFMA (small channel counts: bytes win)
+    t_hbm = conv_bytes_per_step / (PEAK_HBM * 1e9)
+    t_mfma = conv_flop_per_step / (PEAK_BF16 * 1e12)
 
     # HBM bytes of the conv_patch launches of one step, from the committed
     # PMC passes of this configuration (tools/gpu_pmc.sh -> pmc_traffic.json)
@@ -204,13 +212,22 @@ def main():
                                 ("graph per step" if args.no_pipeline else
                                  "graphs, NMS+SORT of step k overlapped with preprocess of step k+1")},
         "roofline": {
-            "kernel": "conv_patch (all YOLOv8n conv launches of a step, HIP events)",
-            "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16,
-            "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 5), "traffic": traffic,
-            "traffic_unit": "bytes per step (all conv_patch launches; PMC, profiles/r01)",
+            "kernel": "conv_patch (all YOLOv8n conv launches of a step, HIP events on the launch "
+                      "stream)",
+            "bound": "hbm" if t_hbm >= t_mfma else "mfma",
+            "achieved": round(achieved_bw if t_hbm >= t_mfma else achieved, 2),
+            "peak": PEAK_HBM if t_hbm >= t_mfma else PEAK_BF16,
+            "unit": "GB/s" if t_hbm >= t_mfma else "TFLOP/s",
+            "frac": round(achieved_bw / PEAK_HBM if t_hbm >= t_mfma else achieved / PEAK_BF16, 5),
+            "traffic": traffic,
+            "traffic_unit": "bytes per step (all conv_patch launches; rocprofv3 PMC FETCH_SIZE x2 "
+                            "+ WRITE_SIZE, profiles/r01/pmc_traffic.json)",
+            "algorithmic_bytes_per_step": round(conv_bytes_per_step),
+            "algorithmic_gflop_per_step": round(conv_flop_per_step / 1e9, 2),
+            "mfma_tflops": round(achieved, 2), "mfma_frac": round(achieved / PEAK_BF16, 5),
+            "hbm_gbs": round(achieved_bw, 1), "hbm_frac": round(achieved_bw / PEAK_HBM, 5),
             "launches_per_step": n_launch,
             "conv_ms_per_step": round(conv_ms_per_step, 4),
-            "conv_gflop_per_step": round(conv_flop_per_step / 1e9, 2),
         },
         "end_to_end_roofline_frac": round(value / world * (BYTES_PER_FRAME / (PEAK_HBM * 1e9) +
                                                            FLOP_PER_FRAME / (PEAK_BF16 * 1e12)), 5),

@@ -165,6 +165,9 @@ int rv_yolo_trace(void* handle, int* recs, int max_recs);
  * algorithmic FLOPs of one launch (2*M*N*K) and the conv index. */
 int rv_yolo_profile(void* handle, int max_forwards);
 int rv_yolo_profile_read(void* handle, double* ms, double* flops, int* conv, int n);
+/* Algorithmic HBM bytes of one launch per conv launch index (inputs read
+ * once, outputs written, residual, weights); returns the entries written. */
+int rv_yolo_profile_bytes(void* handle, double* bytes, int n);
 
 /* Per-layer autotuning of the conv kernels (no reference counterpart: it
  * picks, per conv launch of this handle's forward, the fastest of the valid

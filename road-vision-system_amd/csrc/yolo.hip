@@ -185,6 +185,7 @@ struct Profile {
   int cap_fwd = 0, n_fwd = 0, per_fwd = 0;
   std::vector<hipEvent_t> ev;     // [cap_fwd][per_fwd][2]
   std::vector<double> flops;      // per conv launch index (algorithmic, 2*M*N*K)
+  std::vector<double> bytes;      // per conv launch index (algorithmic HBM bytes, launch_bytes)
   std::vector<int> conv_of;       // conv spec index per launch index
 };
 
@@ -367,6 +368,21 @@ struct Exec {
     M->trace.push_back(r);
   }
 
+  // Algorithmic HBM bytes of one conv launch: every input channel slice it
+  // reads (once), every output / upsampled copy it writes, the residual it
+  // adds and its packed weights -- each byte once, however the kernel tiles.
+  static double launch_bytes(const ConvArgs& a) {
+    const double px_in = (double)a.B * a.Hin * a.Win, px_out = (double)a.B * a.Ho * a.Wo;
+    const bool g2 = a.g2_cout0 > 0;
+    const int cout1 = g2 ? a.g2_cout0 : a.Cout, cout2 = g2 ? a.Cout - a.g2_cout0 : 0;
+    double in_ch = a.Cin;
+    if (g2 && (a.g2_in_co != a.in_co || a.g2_Cin != a.Cin)) in_ch += a.g2_Cin;
+    const double outs = (a.out0 ? (a.out0_up ? 4 : 1) : 0) + (a.out1 ? (a.out1_up ? 4 : 1) : 0);
+    const double w = 2.0 * a.k * a.k * ((double)cout1 * a.Cin + (double)cout2 * (g2 ? a.g2_Cin : 0));
+    return px_in * in_ch * 2 + px_out * a.Cout * (a.out_f32 ? 4 : 2) * outs +
+           (a.res ? px_out * a.Cout * 2 : 0.0) + w;
+  }
+
   static double flops_of(const ConvSpec& c, const ConvArgs& a) {
     return 2.0 * a.B * a.Ho * a.Wo * (double)c.cout * c.cin * c.k * c.k;
   }
@@ -387,6 +403,7 @@ struct Exec {
     if (rec) hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + li_) * 2 + 1], s);
     if (P.on && P.n_fwd == 0 && li_ < P.per_fwd) {
       P.flops[li_] = flops;
+      P.bytes[li_] = launch_bytes(a);
       P.conv_of[li_] = idx;
     }
   }
@@ -725,6 +742,7 @@ extern "C" int rv_yolo_profile(void* h, int max_forwards) {
   P.cap_fwd = max_forwards;
   P.per_fwd = (int)M->def.convs.size();
   P.flops.assign(P.per_fwd, 0.0);
+  P.bytes.assign(P.per_fwd, 0.0);
   P.conv_of.assign(P.per_fwd, -1);
   if (!P.on) return RV_OK;
   P.ev.resize((size_t)P.cap_fwd * P.per_fwd * 2);
@@ -895,4 +913,15 @@ extern "C" int rv_yolo_tuned_config(void* h, int idx, int* cfg5) {
     cfg5[4] = c.persist;
   }
   return (int)M->tuned.size();
+}
+
+// Algorithmic HBM bytes of each conv launch of the profiled forwards (same
+// indexing as rv_yolo_profile_read); returns the number of entries written.
+extern "C" int rv_yolo_profile_bytes(void* h, double* bytes, int n) {
+  RV_CHECK_ARG(h && bytes, "bad args");
+  Model* M = (Model*)h;
+  const Profile& P = M->prof;
+  int k = 0;
+  for (; k < n && k < (int)P.bytes.size(); ++k) bytes[k] = P.bytes[k];
+  return k;
 }

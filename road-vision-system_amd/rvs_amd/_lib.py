@@ -59,6 +59,7 @@ _SIGS = {
     "rv_yolo_trace": (c_int, [c_void_p, c_void_p, c_int]),
     "rv_yolo_profile": (c_int, [c_void_p, c_int]),
     "rv_yolo_profile_read": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
+    "rv_yolo_profile_bytes": (c_int, [c_void_p, c_void_p, c_int]),
     "rv_yolo_autotune": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_int, c_int,
                                  POINTER(c_int), c_void_p]),
     "rv_yolo_tuned_config": (c_int, [c_void_p, c_int, POINTER(c_int)]),
@@ -115,7 +116,8 @@ def check(status: int, what: str = "") -> None:
 
 
 _NOCHECK = {"rv_abi_version", "rv_cand_segments", "rv_yolo_cand_segments", "rv_clahe_median_fits", "rv_clahe_median_letterbox_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
-            "rv_yolo_num_buffers", "rv_yolo_trace", "rv_yolo_profile_read", "rv_yolo_tuned_config"}
+            "rv_yolo_num_buffers", "rv_yolo_trace", "rv_yolo_profile_read", "rv_yolo_tuned_config",
+            "rv_yolo_profile_bytes"}
 
 
 def call(name: str, *args) -> int:

@@ -20,6 +20,8 @@ x = (torch.rand((B, H, W, 3), device="cuda") * 255).to(torch.uint8)
 lb = eng.letterbox(x)
 for _ in range(3):
     eng.forward_raw(lb)
+if not os.environ.get("NO_TUNE"):
+    eng.autotune(lb)
 lib = _lib.load()
 lib.rv_yolo_profile(eng._h, N)
 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -16,7 +16,6 @@ cat "$OUT/bench.json"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
   python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err"
 find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
-find "$OUT/prof" -name "*kernel_trace.csv" -exec cp {} "$OUT/kernel_trace.csv" \;
 rm -rf "$OUT/prof"
 timeout -k 10 200 python3 tools/conv_profile.py > "$OUT/conv_profile.txt" 2>&1
 head -50 "$OUT/conv_profile.txt"
