@@ -88,6 +88,8 @@ def main():
     ap.add_argument("--eager", action="store_true", help="launch kernels eagerly (no HIP graph)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip the per-layer conv kernel autotuning before the timed region")
+    ap.add_argument("--depth", type=int, default=int(os.environ.get("RV_PIPE_DEPTH", 2)),
+                    help="pipelined steps: 3 = Y(k) || P(k+1) || T(k-1), 2 = [T(k-1) || P(k)] -> Y(k)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one graph per step; no overlap of step k's NMS+SORT with step k+1")
     args = ap.parse_args()
@@ -125,7 +127,7 @@ def main():
         # the track stage of step k (NMS + SORT, latency-bound) overlaps the
         # preprocess of step k+1 inside one graph (engine.OverlappedSteps)
         runner = OverlappedSteps(eng, [frames[Wm + k] for k in range(K)],
-                                 [ts_all[Wm + k] for k in range(K)])
+                                 [ts_all[Wm + k] for k in range(K)], depth=args.depth)
         torch.cuda.synchronize()
     elif not args.eager:
         # one HIP graph per timed step (its own frame batch); replayed in order
@@ -210,7 +212,8 @@ def main():
                    "conv_autotune": not args.no_autotune,
                    "execution": "eager" if args.eager else
                                 ("graph per step" if args.no_pipeline else
-                                 "graphs, NMS+SORT of step k overlapped with preprocess of step k+1")},
+                                 f"graphs, {args.depth}-stage software pipeline over steps "
+                                 "(preprocess / YOLO / NMS+SORT of consecutive steps overlap)")},
         "roofline": {
             "kernel": "conv_patch (all YOLOv8n conv launches of a step, HIP events on the launch "
                       "stream)",

@@ -73,7 +73,9 @@ class YoloEngine:
         self.ws_bytes = lib.rv_yolo_ws_bytes(h, self.max_batch)
         dev = self.device
         self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
-        self.lb = torch.empty((self.max_batch, self.in_h, self.in_w, 3), dtype=torch.uint8,
+        # two letterbox slots: a pipelined engine letterboxes frame k+1 while
+        # the forward of frame k still reads its slot
+        self.lb = torch.empty((2, self.max_batch, self.in_h, self.in_w, 3), dtype=torch.uint8,
                               device=dev)
         # segmented candidate layout: nseg segments of 64 rows per image
         self.nseg = lib.rv_yolo_cand_segments(h)
@@ -104,9 +106,9 @@ class YoloEngine:
         except Exception:
             pass
 
-    def letterbox(self, frames: torch.Tensor) -> torch.Tensor:
+    def letterbox(self, frames: torch.Tensor, slot: int = 0) -> torch.Tensor:
         B = frames.shape[0]
-        return kernels.letterbox(frames, self.geo, out=self.lb[:B])
+        return kernels.letterbox(frames, self.geo, out=self.lb[slot][:B])
 
     def forward_raw(self, lb: torch.Tensor, raw: Optional[torch.Tensor] = None,
                     candidates: bool = True, slot: int = 0):

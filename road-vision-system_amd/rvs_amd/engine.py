@@ -60,14 +60,15 @@ class RoadVisionEngine:
         # default chain: CLAHE + median + the detector's LetterBox in one pass
         self.fused_letterbox = self.pipeline.letterbox_fusable(self.H, self.W, self.detector.geo)
 
-    def preprocess_stage(self, frames: torch.Tensor):
+    def preprocess_stage(self, frames: torch.Tensor, lb_slot: int = 0):
         """pipeline(raw) + the detector's LetterBox (main_preview.py:94-99)
-        for (S,H,W,3) u8 device frames -> (proc, letterboxed batch)."""
+        for (S,H,W,3) u8 device frames -> (proc, letterboxed batch in the
+        detector's letterbox slot `lb_slot`)."""
         if self.fused_letterbox:
             return self.pipeline.run_with_letterbox(frames, self.detector.geo,
-                                                    self.detector.lb[:frames.shape[0]])
+                                                    self.detector.lb[lb_slot][:frames.shape[0]])
         proc = self.pipeline(frames)
-        return proc, self.detector.letterbox(proc)
+        return proc, self.detector.letterbox(proc, lb_slot)
 
     def yolo_stage(self, lb: torch.Tensor, slot: int = 0) -> None:
         """YOLOv8 forward + decode; NMS candidates land in candidate slot `slot`."""
@@ -138,40 +139,66 @@ class RoadVisionEngine:
 
 
 class OverlappedSteps:
-    """K captured steps whose latency-bound tail overlaps the next step's head.
+    """K captured steps whose stages overlap across steps.
 
-    The track stage of a step (NMS + SORT: one workgroup per frame / camera
-    stream, so it leaves most of the 256 CUs idle) has no data dependence on
-    the next step's preprocess (CLAHE + median + letterbox of new frames), so
-    graph j runs  [track(j-1) on a side stream  ||  preprocess(j)]  -> join ->
-    yolo(j).  The convs never share the device with another kernel.  Graph 0
-    is preprocess(0) + yolo(0), a last graph runs track(K-1); the two NMS
-    candidate slots alternate by step.  Replayed in order, the K steps give the
-    same results as K step() calls (tests/test_engine_gpu.py)."""
+    A step is three stages with different bottlenecks: preprocess P (CLAHE +
+    median + letterbox: VALU-bound streaming), yolo Y (the conv stack:
+    LDS/MFMA/latency-bound) and track T (NMS + SORT: one workgroup per frame /
+    camera stream, latency-bound and nearly idle on 256 CUs).  Consecutive
+    steps only share state through T (SORT is sequential per stream), so with
+    `depth=3` graph j runs  Y(j) || P(j+1) || T(j-1)  on three streams (the
+    letterbox batch and the NMS candidates are double-buffered by step
+    parity); with `depth=2` it runs  [T(j-1) || P(j)] -> Y(j).  A prologue /
+    epilogue graph fills and drains the pipeline.  Replayed in order, the K
+    steps give the same results as K step() calls (tests/test_engine_gpu.py)."""
 
-    def __init__(self, eng: "RoadVisionEngine", frames, ts):
+    def __init__(self, eng: "RoadVisionEngine", frames, ts, depth: int = 2):
         self.eng = eng
         K = len(frames)
-        side = torch.cuda.Stream(eng.device)
+        dev = eng.device
+        side_t, side_p = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
         self.graphs = []
         self.outs = []
-        for j in range(K + 1):
+        procs = {}
+        if depth == 2:
+            for j in range(K + 1):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    cur = torch.cuda.current_stream()
+                    if j > 0:
+                        side_t.wait_stream(cur)
+                        with torch.cuda.stream(side_t):
+                            out = eng.track_stage(ts[j - 1], (j - 1) % 2)
+                    if j < K:
+                        procs[j], lb = eng.preprocess_stage(frames[j])
+                    if j > 0:
+                        cur.wait_stream(side_t)
+                        out["proc"] = procs.pop(j - 1)
+                        self.outs.append(out)
+                    if j < K:
+                        eng.yolo_stage(lb, j % 2)
+                self.graphs.append(g)
+            return
+        lbs = {}
+        for j in range(-1, K + 1):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 cur = torch.cuda.current_stream()
-                if j > 0:
-                    side.wait_stream(cur)
-                    with torch.cuda.stream(side):
+                side_t.wait_stream(cur)
+                side_p.wait_stream(cur)
+                if j + 1 < K:  # P(j+1) into letterbox slot (j+1) % 2
+                    with torch.cuda.stream(side_p):
+                        procs[j + 1], lbs[j + 1] = eng.preprocess_stage(frames[j + 1], (j + 1) % 2)
+                if j >= 1:  # T(j-1) from candidate slot (j-1) % 2
+                    with torch.cuda.stream(side_t):
                         out = eng.track_stage(ts[j - 1], (j - 1) % 2)
-                if j < K:
-                    proc, lb = eng.preprocess_stage(frames[j])
-                if j > 0:
-                    cur.wait_stream(side)
-                    out["proc"] = self._proc
+                if 0 <= j < K:  # Y(j)
+                    eng.yolo_stage(lbs.pop(j), j % 2)
+                cur.wait_stream(side_p)
+                cur.wait_stream(side_t)
+                if j >= 1:
+                    out["proc"] = procs.pop(j - 1)
                     self.outs.append(out)
-                if j < K:
-                    eng.yolo_stage(lb, j % 2)
-                    self._proc = proc
             self.graphs.append(g)
 
     def run(self):

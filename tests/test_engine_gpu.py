@@ -51,7 +51,8 @@ def test_engine_steps_match_oracle(cuda):
     eng.close()
 
 
-def test_overlapped_steps_match_sequential_steps(cuda):
+@pytest.mark.parametrize("depth", [2, 3])
+def test_overlapped_steps_match_sequential_steps(cuda, depth):
     """bench.py's timed mode (engine.OverlappedSteps): the track stage of step
     k runs on a side stream beside the preprocess of step k+1.  The final
     detections, track ids, proc frames and the whole SORT state must equal
@@ -71,7 +72,8 @@ def test_overlapped_steps_match_sequential_steps(cuda):
         out_seq = seq.step(frames[f], ts[f])
     ovl = RoadVisionEngine(cfg, S, (H, W), device=cuda)
     ovl.step(frames[0], ts[0])  # eager first step (one-time kernel setup)
-    run = OverlappedSteps(ovl, [frames[f] for f in range(1, F)], [ts[f] for f in range(1, F)])
+    run = OverlappedSteps(ovl, [frames[f] for f in range(1, F)], [ts[f] for f in range(1, F)],
+                          depth=depth)
     run.run()
     torch.cuda.synchronize()
     r_seq, r_ovl = seq.results(out_seq), ovl.results(run.outs[-1])
