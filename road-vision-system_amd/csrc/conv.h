@@ -62,6 +62,13 @@ int conv_candidates(const ConvArgs& a, ConvCfg* out, int cap);
 int launch_conv0(const uint8_t* img, int B, int H, int W, const float* w, const float* bias,
                  int C0, bf16_t* out, int out_cs, hipStream_t s);
 
+// conv0 and model.1 (C0 = 16 -> C1 = 32, k3 s2) fused: the P1 map never
+// leaves LDS.  w1/b1: model.1's packed weights / bias; out: X1 (NHWC,
+// channel stride out_cs).
+int launch_stem(const uint8_t* img, int B, int H, int W, const float* w0, const float* b0, int C0,
+                const bf16_t* w1, const float* b1, int C1, bf16_t* out, int out_cs,
+                hipStream_t s);
+
 // SPPF pooling: buf holds x in channels [0, c); writes maxpool5, maxpool5^2
 // and maxpool5^3 (= clipped 5/9/13 windows) into [c,2c), [2c,3c), [3c,4c).
 int launch_sppf_pool(bf16_t* buf, int B, int H, int W, int c, hipStream_t s);

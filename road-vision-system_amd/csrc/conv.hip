@@ -520,7 +520,9 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
       if (c >= nch) break;
       const uint8_t* P = stages + buf * stage_bytes + gi * chunk_bytes;
       const uint8_t* Wl = RESW ? smem + c * W_BYTES : P + g.p_bytes;
-#pragma unroll
+      // kernel rows are not unrolled for the largest tiles: the fragments of
+      // one row (3 taps) in flight keep them under the register file
+#pragma unroll(MR * NR >= 16 ? 1 : K)
       for (int ky = 0; ky < K; ++ky) {
         const uint8_t* Prow = P + ky * g.PW * kPixB;
 #pragma unroll
@@ -701,7 +703,7 @@ constexpr bool patch_s2_ok() {
 // Staged-weight (non-RESW) 3x3 variants with the biggest tiles exceed the
 // register file (scratch spills); they are not built.
 constexpr bool patch_spills(int MR, int NR, int K, int S, bool RESW) {
-  return !RESW && K == 3 && (MR * NR >= 16 || (S == 2 && MR * NR >= 8));
+  return !RESW && K == 3 && ((S == 1 && MR * NR > 16) || (S == 2 && MR * NR >= 8));
 }
 
 template <int MR, int NR, bool RESW>
@@ -998,6 +1000,231 @@ int launch_conv0(const uint8_t* img, int B, int H, int W, const float* w, const 
     return RV_EINVAL;
   }
   return launch_status("conv0");
+}
+
+// ---------------------------------------------------------------------------
+// Fused stem: conv0 (3 -> C0, k3 s2, from the u8 letterbox) and model.1
+// (C0 -> C1, k3 s2) in one kernel; the C0-channel P1 map (X0) only ever
+// lives in LDS.  X0 is the largest activation of the network (B x 192 x 320 x
+// 16 bf16 at 1080p) and model.1 would otherwise read it back with a 3x3
+// halo; here each workgroup computes the X0 pixels its X1 tile needs
+// (halo recomputed, ~13 %) and convolves them straight from LDS.
+//
+// model.1 with C0 = 16 input channels runs on "tap pairs": a 32-deep MFMA
+// k-step takes 16 channels of two horizontally adjacent taps (kx, kx+1),
+// which are two adjacent X0 pixels -- 64 contiguous bytes of the 32-B-per-
+// pixel LDS image -- so a row of taps is 2 k-steps instead of 3 zero-padded
+// ones (the phantom 4th tap has zero weights).  A fragments come straight
+// from the standard packed weights [Cout][ky][kx][32] (L2-resident).
+//
+// Tile: 8 x 32 X1 pixels x 32 couts per workgroup; wave w owns X1 rows 2w,
+// 2w+1 (4 fragments of 16 pixels).  X0 tile: 17 x 66 pixels (the 66th column
+// only feeds the phantom tap).  Letterbox tile: 35 rows x 133 pixels as bf16
+// bit patterns.
+constexpr int kStR = 8, kStC = 32;                      // X1 tile
+constexpr int kStXR = 2 * kStR + 1, kStXC = 2 * kStC + 2;  // X0 tile (17 x 66)
+constexpr int kStLR = 2 * kStXR + 1, kStLC = 2 * kStXC + 1;  // lb tile (35 x 133 px)
+constexpr int kStLS = kStLC * 3 + 5;                    // lb row stride (u16), 404
+constexpr int kStXB = kStXR * kStXC * 32;               // X0 tile bytes (35,904)
+constexpr int kStLB = kStLR * kStLS * 2;                // lb tile bytes (28,280)
+
+__global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ img, int B, int H,
+                                                   int W, const float* __restrict__ w0,
+                                                   const float* __restrict__ b0,
+                                                   const uint16_t* __restrict__ w1,
+                                                   const float* __restrict__ b1,
+                                                   uint16_t* __restrict__ out, int out_cs) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* xs = smem;                               // X0 tile: [17][66] px x 32 B
+  uint16_t* ls = (uint16_t*)(smem + kStXB);         // lb tile: [35][404] u16
+  const int H0 = (H + 1) / 2, W0 = (W + 1) / 2;     // X0 map
+  const int H1 = (H0 + 1) / 2, W1 = (W0 + 1) / 2;   // X1 map
+  const int tiles_x = (W1 + kStC - 1) / kStC, tiles_y = (H1 + kStR - 1) / kStR;
+  int bid = blockIdx.x;
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int b = bid / tiles_y;
+  const int oy0 = ty * kStR, ox0 = tx * kStC;        // X1 tile origin
+  const int xy0 = 2 * oy0 - 1, xx0 = 2 * ox0 - 1;    // X0 tile origin
+  const int ly0 = 2 * xy0 - 1, lx0 = 2 * xx0 - 1;    // lb tile origin (pixels)
+  const uint8_t* frame = img + (size_t)b * H * W * 3;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
+
+  // ---- 1. letterbox tile -> LDS as bf16 bit patterns (0 outside the image)
+  {
+    constexpr int kDw = (kStLC * 3 + 1 + 3) / 4;       // dwords per row (covers 399 B + 1)
+    constexpr int kN = kStLR * kDw;
+    const int bx0 = lx0 * 3;
+    const bool aligned_rows = (W * 3) % 4 == 0 && ((uintptr_t)frame & 3) == 0;
+    for (int i0 = tid; i0 < kN; i0 += 4 * 256) {
+      uint32_t dv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 256;
+        dv[u] = 0;
+        if (i < kN) {
+          const int r = i / kDw, d = i - (i / kDw) * kDw;
+          const int iy = ly0 + r, a = bx0 - 1 + 4 * d;  // first byte of this word
+          if ((unsigned)iy < (unsigned)H) {
+            const uint8_t* row = frame + (size_t)iy * W * 3;
+            if (aligned_rows && a >= 0 && a + 3 < W * 3) {
+              dv[u] = *(const uint32_t*)(row + a);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (a + q >= 0 && a + q < W * 3) dv[u] |= (uint32_t)row[a + q] << (8 * q);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 256;
+        if (i < kN) {
+          const int r = i / kDw, d = i - (i / kDw) * kDw;
+          const uint32_t f0 = __float_as_uint((float)(dv[u] & 255));
+          const uint32_t f1 = __float_as_uint((float)((dv[u] >> 8) & 255));
+          const uint32_t f2 = __float_as_uint((float)((dv[u] >> 16) & 255));
+          const uint32_t f3 = __float_as_uint((float)(dv[u] >> 24));
+          uint32_t* dst = (uint32_t*)(ls + r * kStLS + 4 * d);  // element e = byte column e - 1
+          dst[0] = (f0 >> 16) | (f1 & 0xFFFF0000u);
+          dst[1] = (f2 >> 16) | (f3 & 0xFFFF0000u);
+        }
+      }
+    }
+  }
+  // conv0 weights: A rows cout = col, k = 8*quad + j over (ky, kx, ch) with
+  // BGR -> RGB and 1/255 folded in, split hi + mid + lo bf16 (as conv0_kernel)
+  bf16x8 Ah, Am, Al;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * quad + j;
+    float v = 0.f;
+    if (k < 27) {
+      const int ky = k / 9, rem = k - ky * 9, kx = rem / 3, ch = rem - kx * 3;
+      v = w0[((col * 3 + (2 - ch)) * 3 + ky) * 3 + kx] / 255.0f;
+    }
+    const __bf16 hi = (__bf16)v;
+    const float r1 = v - (float)hi;
+    const __bf16 mid = (__bf16)r1;
+    Ah[j] = hi;
+    Am[j] = mid;
+    Al[j] = (__bf16)(r1 - (float)mid);
+  }
+  float bias0[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias0[i] = b0[4 * quad + i];
+  int koff[8];  // lb tile element offsets of this lane's 8 k values (pixel 0, 0)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * quad + j;
+    const int kk = k < 27 ? k : 0;  // padded k: any value, its weight is 0
+    const int ky = kk / 9, rem = kk - ky * 9;
+    koff[j] = ky * kStLS + rem + 1;  // element = byte column + 1
+  }
+  __syncthreads();
+
+  // ---- 2. conv0 for the X0 tile (17 x 66 pixels, 16-pixel fragments)
+  constexpr int kXpx = kStXR * kStXC;                // 1122
+  constexpr int kXfr = (kXpx + 15) / 16;             // 71
+  for (int f = wave; f < kXfr; f += 4) {
+    const int i = f * 16 + col;                      // X0 tile pixel of this lane (B column)
+    const int ii = i < kXpx ? i : 0;
+    const int yr = ii / kStXC, xr = ii - (ii / kStXC) * kStXC;
+    const int base = 2 * yr * kStLS + 2 * xr * 3;
+    bf16x8 X;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) X[j] = __builtin_bit_cast(__bf16, ls[base + koff[j]]);
+    f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, X, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, X, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, X, acc, 0, 0, 0);
+    // lane holds couts 4*quad .. 4*quad+3 of pixel i; outside the X0 map the
+    // value is model.1's zero padding
+    const int gy = xy0 + yr, gx = xx0 + xr;
+    const bool inside = i < kXpx && (unsigned)gy < (unsigned)H0 && (unsigned)gx < (unsigned)W0;
+    uint2 pk = make_uint2(0, 0);
+    if (inside)
+      pk = make_uint2(pack_bf16x2(silu(acc[0] + bias0[0]), silu(acc[1] + bias0[1])),
+                      pack_bf16x2(silu(acc[2] + bias0[2]), silu(acc[3] + bias0[3])));
+    if (i < kXpx) *(uint2*)(xs + i * 32 + quad * 8) = pk;
+  }
+  __syncthreads();
+
+  // ---- 3. model.1 (C0 = 16 -> 32, k3 s2) on tap pairs from the X0 tile
+  constexpr int MR = 2, NR = 4;
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // this lane's B column: X1 pixel (row 2*wave + n/2, col (n&1)*16 + col)
+  int bbase[NR];
+#pragma unroll
+  for (int n = 0; n < NR; ++n) {
+    const int r = 2 * wave + (n >> 1), c = (n & 1) * 16 + col;
+    bbase[n] = ((2 * r) * kStXC + 2 * c) * 32 + quad * 16;
+  }
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      bf16x8 A[MR], Bf[NR];
+      const int kx = 2 * p + (quad >> 1);  // quads 0,1: tap 2p; quads 2,3: tap 2p+1
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        const int co = m * 16 + col;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (kx < 3) v = *(const uint4*)(w1 + ((size_t)co * 9 + ky * 3 + kx) * 32 + (quad & 1) * 8);
+        A[m] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int n = 0; n < NR; ++n)
+        Bf[n] = __builtin_bit_cast(bf16x8, *(const uint4*)(xs + bbase[n] + (ky * kStXC + 2 * p) * 32));
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int n = 0; n < NR; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[m], Bf[n], acc[m][n], 0, 0, 0);
+    }
+  // epilogue: bias + SiLU -> X1 (bf16 NHWC, channel stride out_cs)
+#pragma unroll
+  for (int n = 0; n < NR; ++n) {
+    const int oy = oy0 + 2 * wave + (n >> 1), ox = ox0 + (n & 1) * 16 + col;
+    if (oy >= H1 || ox >= W1) continue;
+    uint16_t* o = out + (((size_t)b * H1 + oy) * W1 + ox) * out_cs;
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      const int co = m * 16 + quad * 4;
+      const f32x4 bb = *(const f32x4*)(b1 + co);
+      *(uint2*)(o + co) = make_uint2(pack_bf16x2(silu(acc[m][n][0] + bb[0]), silu(acc[m][n][1] + bb[1])),
+                                     pack_bf16x2(silu(acc[m][n][2] + bb[2]), silu(acc[m][n][3] + bb[3])));
+    }
+  }
+}
+
+int launch_stem(const uint8_t* img, int B, int H, int W, const float* w0, const float* b0, int C0,
+                const bf16_t* w1, const float* b1, int C1, bf16_t* out, int out_cs,
+                hipStream_t s) {
+  if (C0 != 16 || C1 != 32) {
+    set_error("stem: C0=%d C1=%d (fused stem needs 16 -> 32)", C0, C1);
+    return RV_EINVAL;
+  }
+  const int H0 = (H + 1) / 2, W0 = (W + 1) / 2;
+  const int H1 = (H0 + 1) / 2, W1 = (W0 + 1) / 2;
+  const int blocks = B * ceil_div(H1, kStR) * ceil_div(W1, kStC);
+  const size_t smem = (size_t)kStXB + kStLB;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)stem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    (void)hipGetLastError();
+    attr = true;
+  }
+  stem_kernel<<<blocks, 256, smem, s>>>(img, B, H, W, w0, b0, (const uint16_t*)w1, b1,
+                                        (uint16_t*)out, out_cs);
+  return launch_status("stem");
 }
 
 // ---------------------------------------------------------------------------

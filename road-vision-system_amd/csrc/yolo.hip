@@ -202,6 +202,16 @@ struct Model {
     return -1;
   }
   const uint8_t* dev = nullptr;  // packed weights (caller-owned device memory)
+  // side streams + events for the forked P3 / P4 Detect heads
+  hipStream_t side[2] = {nullptr, nullptr};
+  hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
+  ~Model() {
+    for (int i = 0; i < 2; ++i) {
+      if (side[i]) hipStreamDestroy(side[i]);
+      if (ev_fork[i]) hipEventDestroy(ev_fork[i]);
+      if (ev_join[i]) hipEventDestroy(ev_join[i]);
+    }
+  }
   int max_B = 0, H = 0, W = 0;
   std::vector<Buf> bufs;
   int nA = 0;
@@ -556,6 +566,14 @@ extern "C" int rv_yolo_create(int variant, const void* dev_packed, int max_B, in
     return RV_EINVAL;
   }
   M->dev = (const uint8_t*)dev_packed;
+  for (int i = 0; i < 2; ++i) {
+    if (hipStreamCreateWithFlags(&M->side[i], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&M->ev_fork[i], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&M->ev_join[i], hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      M->side[0] = M->side[1] = nullptr;  // sequential heads
+    }
+  }
   M->max_B = max_B;
   M->H = in_h;
   M->W = in_w;
@@ -610,11 +628,29 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   M->launches.clear();
   // backbone
   const ConvSpec& c0 = M->def.convs[0];
-  int st = launch_conv0(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
-                        (const float*)(M->dev + c0.b_off), c0.cout, (bf16_t*)E.ptr(M->X0), v.c1,
-                        E.s);
-  if (st) return st;
-  E.conv("model.1", View{M->X0, v.c1, 0}, 1, View{M->X1, v.c2, 0});
+  // conv0 + model.1 fused (the P1 map stays in LDS) unless the caller asked
+  // for the raw prediction (parity / debug forwards keep every activation
+  // in the workspace) or RV_FUSE_STEM=0
+  static const bool stem_env = !getenv("RV_FUSE_STEM") || atoi(getenv("RV_FUSE_STEM")) != 0;
+  const int i1 = M->def.find("model.1");
+  const bool fuse_stem = stem_env && !raw_out && c0.cout == 16 && v.c2 == 32 && i1 >= 0;
+  int st;
+  if (fuse_stem) {
+    const ConvSpec& c1 = M->def.convs[i1];
+    const View none{-1, 0, 0};
+    E.trace(i1, E.args(c1, View{M->X0, v.c1, 0}, 1, View{M->X1, v.c2, 0}, 0, none, 0, none),
+            View{M->X0, v.c1, 0}, View{M->X1, v.c2, 0}, 0, none, 0, none);
+    st = launch_stem(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
+                     (const float*)(M->dev + c0.b_off), c0.cout, E.wptr(c1), E.bptr(c1), c1.cout,
+                     (bf16_t*)E.ptr(M->X1), v.c2, E.s);
+    if (st) return st;
+  } else {
+    st = launch_conv0(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
+                      (const float*)(M->dev + c0.b_off), c0.cout, (bf16_t*)E.ptr(M->X0), v.c1,
+                      E.s);
+    if (st) return st;
+    E.conv("model.1", View{M->X0, v.c1, 0}, 1, View{M->X1, v.c2, 0});
+  }
   E.c2f("model.2", View{M->X1, v.c2, 0}, 2, M->C2, v.c2, v.nb, true, View{M->X2, v.c2, 0});
   E.conv("model.3", View{M->X2, v.c2, 0}, 2, View{M->X3, v.c3, 0});
   const int cat14 = v.h12 + v.c3, cat11 = v.c5 + v.c4, cat20 = v.h18 + v.c5,
@@ -637,23 +673,21 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   // head
   E.c2f("model.12", View{M->CAT11, cat11, 0}, 4, M->C12, v.h12, v.nb, false,
         View{M->CAT17, cat17, v.h15}, 0, View{M->CAT14, cat14, 0}, 1);
-  E.c2f("model.15", View{M->CAT14, cat14, 0}, 3, M->C15, v.h15, v.nb, false,
-        View{M->X15, v.h15, 0});
-  E.conv("model.16", View{M->X15, v.h15, 0}, 3, View{M->CAT17, cat17, 0});
-  E.c2f("model.18", View{M->CAT17, cat17, 0}, 4, M->C18, v.h18, v.nb, false,
-        View{M->X18, v.h18, 0});
-  E.conv("model.19", View{M->X18, v.h18, 0}, 4, View{M->CAT20, cat20, 0});
-  E.c2f("model.21", View{M->CAT20, cat20, 0}, 5, M->C21, v.h21, v.nb, false,
-        View{M->X21, v.h21, 0});
-  // Detect
+  // Detect head of level i: box (cv2) and class (cv3) branches, one grouped
+  // launch per stage; the last 1x1 stage runs inside the decode kernel
+  // (RV_FUSE_HEAD=0: separate launches and f32 logits in HBM).  The P3 and
+  // P4 heads are forked onto side streams as soon as their input map exists,
+  // so they overlap the rest of the neck (small, latency-bound launches);
+  // RV_HEAD_STREAMS=0 keeps everything on the caller's stream.
   const View P[3] = {View{M->X15, v.h15, 0}, View{M->X18, v.h18, 0}, View{M->X21, v.h21, 0}};
   const int dcs = v.c2d + v.c3d, hcs = 4 * v.reg + v.nc;
-  // box (cv2) and class (cv3) branches of a level: one grouped launch per
-  // stage; the last 1x1 stage runs inside the decode kernel (RV_FUSE_HEAD=0:
-  // separate launches and f32 logits in HBM)
   static const bool fuse_env = !getenv("RV_FUSE_HEAD") || atoi(getenv("RV_FUSE_HEAD")) != 0;
   const bool fuse_head = fuse_env && v.c2d % 8 == 0 && v.c3d % 8 == 0;
-  for (int i = 0; i < 3; ++i) {
+  static const bool streams_env =
+      !getenv("RV_HEAD_STREAMS") || atoi(getenv("RV_HEAD_STREAMS")) != 0;
+  const bool fork = streams_env && M->side[0] && M->side[1];
+  const hipStream_t main_s = E.s;
+  auto head_level = [&](int i) {
     const std::string a = "model.22.cv2." + std::to_string(i), c = "model.22.cv3." + std::to_string(i);
     E.conv_pair(a + ".0", P[i], c + ".0", P[i], 3 + i, View{M->DA[i], dcs, 0});
     E.conv_pair(a + ".1", View{M->DA[i], dcs, 0}, c + ".1", View{M->DA[i], dcs, v.c2d}, 3 + i,
@@ -673,7 +707,31 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
                          none, 0, none),
               View{M->DB[i], dcs, v.c2d}, View{M->HD[i], hcs, 4 * v.reg}, 0, none, 0, none);
     }
-  }
+    return E.status;
+  };
+  auto forked_head = [&](int i) {  // level i's head on side stream i (joined before decode)
+    if (!fork) return head_level(i);
+    hipEventRecord(M->ev_fork[i], main_s);
+    hipStreamWaitEvent(M->side[i], M->ev_fork[i], 0);
+    E.s = M->side[i];
+    const int r = head_level(i);
+    hipEventRecord(M->ev_join[i], M->side[i]);
+    E.s = main_s;
+    return r;
+  };
+  E.c2f("model.15", View{M->CAT14, cat14, 0}, 3, M->C15, v.h15, v.nb, false,
+        View{M->X15, v.h15, 0});
+  if (E.status || forked_head(0)) return E.status;
+  E.conv("model.16", View{M->X15, v.h15, 0}, 3, View{M->CAT17, cat17, 0});
+  E.c2f("model.18", View{M->CAT17, cat17, 0}, 4, M->C18, v.h18, v.nb, false,
+        View{M->X18, v.h18, 0});
+  if (E.status || forked_head(1)) return E.status;
+  E.conv("model.19", View{M->X18, v.h18, 0}, 4, View{M->CAT20, cat20, 0});
+  E.c2f("model.21", View{M->CAT20, cat20, 0}, 5, M->C21, v.h21, v.nb, false,
+        View{M->X21, v.h21, 0});
+  if (E.status || head_level(2)) return E.status;
+  if (fork)
+    for (int i = 0; i < 2; ++i) hipStreamWaitEvent(main_s, M->ev_join[i], 0);
   if (E.status) return E.status;
   if (M->prof.on && M->prof.n_fwd < M->prof.cap_fwd) M->prof.n_fwd++;
   HeadLevel hl[3];

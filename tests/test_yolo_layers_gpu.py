@@ -198,3 +198,26 @@ def test_autotuned_configs_are_bit_identical(cuda):
     eng.forward_raw(lb, raw1)
     np.testing.assert_array_equal(raw1.cpu().numpy(), raw0.cpu().numpy())
     eng.close()
+
+
+def test_fused_stem_matches_unfused(cuda):
+    """conv0 + model.1 fused (X0 kept in LDS, model.1 on tap pairs) against
+    the unfused pair: same X0 values, model.1 accumulated in another k order,
+    so X1 agrees to 1 bf16 ulp (fewer than 1e-4 of the elements beyond)."""
+    from rvs_amd.detect import weights
+    from rvs_amd.detect.yolo_hip import YoloEngine
+    H, W, B = 1080, 1920, 2
+    eng = YoloEngine(0, weights.synthetic_weights(0, seed=3), B, (H, W), device=cuda)
+    fr = np.stack([cpu.median(cpu.clahe_ycrcb(road_frame(H, W, seed=70 + b)), 3) for b in range(B)])
+    lb = eng.letterbox(torch.from_numpy(fr).to(cuda))
+    eng.forward_raw(lb)  # no raw output: fused stem
+    x1_fused = Introspect(eng, B).view(1).copy()
+    raw = torch.empty((B, 84, eng.A), dtype=torch.float32, device=cuda)
+    eng.forward_raw(lb, raw)  # raw output requested: conv0 + model.1 separately
+    x1 = Introspect(eng, B).view(1)
+    assert x1.shape == (B, 96, 160, 32)
+    rms = float(np.sqrt(np.mean(x1.astype(np.float64) ** 2))) + 1e-12
+    d = np.abs(x1_fused.astype(np.float64) - x1)
+    assert float((d > ulp_bf16(x1) * 1.01 + 1e-3 * rms).mean()) < 1e-4
+    assert (d <= 2 * ulp_bf16(x1) + 1e-2 * rms).all()
+    eng.close()
