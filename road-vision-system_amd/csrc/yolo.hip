@@ -685,7 +685,10 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   const bool fuse_head = fuse_env && v.c2d % 8 == 0 && v.c3d % 8 == 0;
   static const bool streams_env =
       !getenv("RV_HEAD_STREAMS") || atoi(getenv("RV_HEAD_STREAMS")) != 0;
-  const bool fork = streams_env && M->side[0] && M->side[1];
+  // profiled forwards time every launch alone (per-launch roofline), so the
+  // heads stay on the caller's stream there
+  const bool fork = streams_env && M->side[0] && M->side[1] &&
+                    !(M->prof.on && M->prof.n_fwd < M->prof.cap_fwd);
   const hipStream_t main_s = E.s;
   auto head_level = [&](int i) {
     const std::string a = "model.22.cv2." + std::to_string(i), c = "model.22.cv3." + std::to_string(i);
