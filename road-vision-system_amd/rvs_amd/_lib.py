@@ -14,6 +14,11 @@ from ctypes import c_double, c_float, c_int, c_size_t, c_void_p, POINTER
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "librvhip.so")
+# A/B runs of two builds on one box (tools/ab_env.sh): RV_LIB_VARIANT=x loads
+# librvhip_x.so from this directory instead ("default" or unset: librvhip.so).
+_variant = os.environ.get("RV_LIB_VARIANT", "default")
+if _variant != "default":
+    LIB_PATH = os.path.join(_HERE, "librvhip_%s.so" % _variant)
 
 _lib = None
 
