@@ -360,21 +360,28 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[MR][NR]
   }
 }
 
-// Patch layout in LDS: pixel pp of the halo patch owns 80 bytes at pp * 80
-// (its 32 channels = 4 x 16-B quarters + one 16-B pad slot).  The 80-B
-// stride makes the 16 pixels of a B fragment hit 16 disjoint 4-bank groups
-// (20 dwords apart), so a fragment read needs no swizzle and every tap's
-// address is the pixel's base plus a compile-time/uniform offset.  The DMA
-// stays lane-linear: lane l of DMA instruction j fills slot L = 64 j + l,
-// i.e. pixel L / 5, quarter L % 5 (quarter 4 = pad, fetched from the zero
-// block).
-constexpr int kPixB = 80;
+// Patch layout in LDS.  Stride-1 convs: pixel pp of the halo patch owns 64
+// bytes at pp * 64 (its 32 channels = 4 x 16-B quarters); LDS slot quarter
+// q of a pixel in patch column px holds source quarter q ^ ((px >> 2) & 3),
+// so the 16 consecutive pixels of a B fragment (one patch row) hit 16
+// disjoint 4-bank groups.  The swizzle depends on the column only, so a
+// kernel-row step (ky) moves every address by the same PW * 64 and the
+// per-lane tap addresses are precomputed once per block (NR x K values).
+// Stride-2 convs (fragment pixels two columns apart) use an 80-B stride
+// instead (4 quarters + a pad slot from the zero block): 16 pixels 40 dwords
+// apart are again disjoint, with no swizzle.  The DMA stays lane-linear:
+// lane l of DMA instruction j fills slot L = 64 j + l, i.e. pixel L / SL,
+// slot quarter L % SL (SL = 4 or 5 slots per pixel).
+template <int S>
+constexpr int patch_pixb() {
+  return S == 1 ? 64 : 80;
+}
 
 // Per-lane DMA source offsets of one patch (elements from the image base,
 // -1 = zero block), at most patch_maxit(NR, S) DMA instructions per wave.
 template <int NR, int S>
 constexpr int patch_maxit() {
-  return (S == 2 ? 6 : 3) * NR + 2;
+  return (S == 2 ? 6 : 2) * NR + 2;
 }
 
 // Persistent, software-pipelined form: the block owns cout tile blockIdx.y
@@ -437,7 +444,8 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
   const float inv_pw = 1.0f / (float)g.PW;
 
   // block-constant: output slots -> (r, cc) of the tile, patch byte base
-  int orow[NR], ocol[NR], pb80[NR];
+  constexpr int PB = patch_pixb<S>(), SL = PB / 16;
+  int orow[NR], ocol[NR], boff[NR][K];
   bool oin[NR];
 #pragma unroll
   for (int n = 0; n < NR; ++n) {
@@ -445,7 +453,14 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
     orow[n] = q / g.C;
     ocol[n] = q - orow[n] * g.C;
     oin[n] = q < g.R * g.C;
-    pb80[n] = (oin[n] ? (orow[n] * S) * g.PW + ocol[n] * S : 0) * kPixB + quad * 16;
+    // per-lane LDS byte address of tap (0, kx) for output slot n
+    const int pr = oin[n] ? orow[n] * S : 0, pc = oin[n] ? ocol[n] * S : 0;
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx) {
+      const int pp = pr * g.PW + pc + kx;
+      boff[n][kx] = PB == 64 ? pp * 64 + ((quad ^ (((pc + kx) >> 2) & 3)) << 4)
+                             : pp * PB + quad * 16;
+    }
   }
   f32x4 bias[MR];
 #pragma unroll
@@ -466,14 +481,15 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
 #pragma unroll
     for (int it = 0; it < MAXP; ++it) {
       const int L = 64 * (wave + 4 * it) + lane;
-      const int pix = L / 5, q = L - 5 * pix;
+      const int pix = L / SL, q = L - SL * pix;
       const int py = (int)(((float)pix + 0.5f) * inv_pw);
       const int px = pix - py * g.PW;
       const int iy = iy0 + py, ix = ix0 + px;
-      const bool ok = q < 4 && pix < npp && (unsigned)iy < (unsigned)a.Hin &&
+      const int sq = PB == 64 ? q ^ ((px >> 2) & 3) : q;  // source quarter of slot q
+      const bool ok = sq < 4 && pix < npp && (unsigned)iy < (unsigned)a.Hin &&
                       (unsigned)ix < (unsigned)a.Win;
-      poff[it] = ok ? (iy * a.Win + ix) * a.in_cs + q * 8 : -1;
-      if ((nch - 1) * 32 + q * 8 >= Cin) tailbad |= 1u << it;
+      poff[it] = ok ? (iy * a.Win + ix) * a.in_cs + sq * 8 : -1;
+      if ((nch - 1) * 32 + sq * 8 >= Cin) tailbad |= 1u << it;
     }
   };
   // weight DMA: instruction j moves (row, tap) pairs 16 j .. 16 j + 15, a
@@ -524,7 +540,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
       // one row (3 taps) in flight keep them under the register file
 #pragma unroll(MR * NR >= 16 ? 1 : K)
       for (int ky = 0; ky < K; ++ky) {
-        const uint8_t* Prow = P + ky * g.PW * kPixB;
+        const uint8_t* Prow = P + ky * g.PW * PB;
 #pragma unroll
         for (int kx = 0; kx < K; ++kx) {
           const int tap = ky * K + kx;
@@ -537,7 +553,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
           }
 #pragma unroll
           for (int n = 0; n < NR; ++n)
-            Bf[n] = __builtin_bit_cast(bf16x8, *(const uint4*)(Prow + pb80[n] + kx * kPixB));
+            Bf[n] = __builtin_bit_cast(bf16x8, *(const uint4*)(Prow + boff[n][kx]));
 #pragma unroll
           for (int m = 0; m < MR; ++m)
 #pragma unroll
@@ -621,14 +637,14 @@ static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& 
   if (g.R < 1) return false;
   g.PH = (g.R - 1) * a.stride + a.k;
   g.PW = (g.C - 1) * a.stride + a.k;
-  g.pinst = ceil_div(g.PH * g.PW * 5, 64);  // 5 x 16-B slots per pixel (kPixB)
+  g.pinst = ceil_div(g.PH * g.PW * (a.stride == 1 ? 4 : 5), 64);  // 16-B slots (patch_pixb)
   g.p_bytes = g.pinst * 1024;
   g.tiles_x = ceil_div(a.Wo, g.C);
   g.tiles_y = ceil_div(a.Ho, g.R);
   const int nch = conv_nch(a);
   g.G = std::max(1, std::min(c.G, nch));
   // per-lane offset registers of the kernel (patch_maxit)
-  const int maxit = (a.stride == 2 ? 6 : 3) * NR + 2;
+  const int maxit = (a.stride == 2 ? 6 : 2) * NR + 2;
   if (ceil_div(g.pinst, 4) > maxit) return false;
   const size_t wb = (size_t)16 * MR * a.k * a.k * 64;
   // two stages: the next (tile, chunk group) streams in during the current one
