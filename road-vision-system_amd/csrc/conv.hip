@@ -620,17 +620,19 @@ static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& 
   if (!((a.k == 1 || a.k == 3) && (a.stride == 1 || a.stride == 2) && a.pad == a.k / 2)) return false;
   const int NR = c.nr, MR = c.mr;
   const int P = 64 * NR;
-  int C;
-  if (a.Wo <= P && a.Wo <= 64) {
-    C = a.Wo;
-  } else {
-    C = 16;
-    for (int cc : {64, 32, 16})
-      if (cc <= P && a.Wo % cc == 0) {
-        C = cc;
-        break;
-      }
-    if (a.Wo % C != 0) C = P >= 32 ? 32 : 16;
+  // tile width: the fewest halo-patch pixels DMA'd over the whole layer
+  // (tiles x PH x PW, edge tiles included); at least 16 columns, so a B
+  // fragment's 16 pixels mostly share one patch row (conflict-free reads)
+  int C = 0;
+  long best = -1;
+  for (int c = std::min(std::min(a.Wo, P), 64 * NR); c >= std::min(16, a.Wo); --c) {
+    const int r = P / c;
+    const long cost = (long)ceil_div(a.Wo, c) * ceil_div(a.Ho, r) * ((r - 1) * a.stride + a.k) *
+                      ((c - 1) * a.stride + a.k);
+    if (best < 0 || cost < best) {
+      best = cost;
+      C = c;
+    }
   }
   g.C = C;
   g.R = P / C;
