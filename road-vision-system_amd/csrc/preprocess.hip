@@ -52,13 +52,16 @@ static ClaheGeo make_geo(int H, int W, int tiles, double clip) {
 
 // ---------------------------------------------------------------------------
 // Kernel A: per (tile, frame) histogram of Y -> clip -> redistribute -> LUT.
-// One 256-thread workgroup per tile; 4 per-wave LDS histograms cut atomic
-// contention on low-contrast tiles.
+// One 256-thread workgroup per tile.  16 LDS histogram copies (wave x lane
+// & 3), bin-major so the copies of one bin sit in 16 different banks: equal
+// Y values in a wave (flat sky / asphalt) spread over 4 addresses instead of
+// serialising on one, with no bank conflicts between the copies.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restrict__ in,
                                                         uint8_t* __restrict__ lut, int H, int W,
                                                         int pitch, ClaheGeo g) {
-  __shared__ int hist[4][256];
+  constexpr int kCopies = 16;
+  __shared__ int hist[256 * kCopies];
   __shared__ int scan[256];
   __shared__ int wsum[4];
   const int t = threadIdx.x;
@@ -69,13 +72,13 @@ __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restric
   const int x0 = tx * g.tw, y0 = ty * g.th;
   const uint8_t* frame = in + (size_t)b * H * pitch;
 
-  for (int i = t; i < 4 * 256; i += 256) (&hist[0][0])[i] = 0;
+  for (int i = t; i < kCopies * 256; i += 256) hist[i] = 0;
   __syncthreads();
 
   const bool inside = (x0 + g.tw <= W) && (y0 + g.th <= H);
   const bool vec = inside && (g.tw % 4 == 0) && (pitch % 4 == 0) &&
                    ((((uintptr_t)frame) + (uintptr_t)x0 * 3) % 4 == 0);
-  int* h = hist[wave];
+  int* h = hist + ((wave << 2) | (t & 3));  // bin y -> h[y * kCopies]
   if (vec) {
     const int groups = g.tw >> 2;
     const int total = groups * g.th;
@@ -101,10 +104,10 @@ __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restric
         if (i0 + u * 256 >= total) break;
         const uint32_t w0 = w[u][0], w1 = w[u][1], w2 = w[u][2];
         // bytes little-endian: w0 = b0 g0 r0 b1 | w1 = g1 r1 b2 g2 | w2 = r2 b3 g3 r3
-        atomicAdd(&h[bgr_to_y(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255)], 1);
-        atomicAdd(&h[bgr_to_y(w0 >> 24, w1 & 255, (w1 >> 8) & 255)], 1);
-        atomicAdd(&h[bgr_to_y((w1 >> 16) & 255, w1 >> 24, w2 & 255)], 1);
-        atomicAdd(&h[bgr_to_y((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24)], 1);
+        atomicAdd(&h[bgr_to_y(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255) * kCopies], 1);
+        atomicAdd(&h[bgr_to_y(w0 >> 24, w1 & 255, (w1 >> 8) & 255) * kCopies], 1);
+        atomicAdd(&h[bgr_to_y((w1 >> 16) & 255, w1 >> 24, w2 & 255) * kCopies], 1);
+        atomicAdd(&h[bgr_to_y((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24) * kCopies], 1);
       }
     }
   } else {
@@ -117,12 +120,14 @@ __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restric
       int sx = x0 + c;
       if (sx >= W) sx = reflect101(sx, W);
       const uint8_t* p = frame + (size_t)sy * pitch + (size_t)sx * 3;
-      atomicAdd(&h[bgr_to_y(p[0], p[1], p[2])], 1);
+      atomicAdd(&h[bgr_to_y(p[0], p[1], p[2]) * kCopies], 1);
     }
   }
   __syncthreads();
 
-  int v = hist[0][t] + hist[1][t] + hist[2][t] + hist[3][t];
+  int v = 0;
+#pragma unroll
+  for (int c = 0; c < kCopies; ++c) v += hist[t * kCopies + ((c + t) & (kCopies - 1))];
   if (g.clip_limit > 0) {
     int ex = v > g.clip_limit ? v - g.clip_limit : 0;
     v = v > g.clip_limit ? g.clip_limit : v;
