@@ -178,9 +178,10 @@ int rv_yolo_profile_bytes(void* handle, double* bytes, int n);
  * *n_bad counts the ones that were not.  reps: timed launches per config. */
 int rv_yolo_autotune(void* handle, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
                      int reps, int verify, int* n_bad, void* stream);
-/* cfg5 = {MR, NR, G, resw, persist} of conv launch idx (MR 0 = default
+/* cfg6 = {MR, NR, G, resw, persist, kind} of conv launch idx (kind 0: LDS-staged
+ * patch kernel, 1: direct-B 1x1 kernel; MR 0 = default
  * heuristic); returns the number of tuned launches (0 before autotuning). */
-int rv_yolo_tuned_config(void* handle, int idx, int* cfg5);
+int rv_yolo_tuned_config(void* handle, int idx, int* cfg6);
 
 /* --- Ultralytics non_max_suppression + scale_boxes + class filter
  * (yolo_ultralytics.py:28-53), one workgroup per image. */

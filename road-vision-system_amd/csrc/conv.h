@@ -45,6 +45,7 @@ struct ConvArgs {
 // weights, persistent grid.
 struct ConvCfg {
   int mr, nr, G, resw, persist;
+  int kind = 0;  // 0: LDS-staged patch kernel; 1: 1x1 direct-B kernel (G, resw unused)
 };
 
 // Implicit-GEMM conv on MFMA (v_mfma_f32_16x16x32_bf16), default config.

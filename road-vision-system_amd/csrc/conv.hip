@@ -609,6 +609,124 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// conv1x1_direct_kernel: 1x1 stride-1 convs without LDS staging of the
+// pixels.  A 1x1 conv has no halo, so an input pixel feeds exactly one B
+// fragment column: each lane loads its 16-B fragment slice straight from
+// HBM/L2 into VGPRs (global_load_dwordx4), and chunk c+1's loads are in
+// flight while chunk c runs on MFMA -- no LDS round trip and no barrier in
+// the K loop.  The block's weights (16*MR couts x Cin) are DMA'd into LDS
+// once (same per-chunk layout and quarter swizzle as the patch kernel) and
+// stay resident while a persistent block walks its pixel tiles (64*NR
+// consecutive NHWC pixels of the flattened B x H x W range).  The k order
+// (chunks ascending, 32 channels per MFMA) equals the patch kernel's, so the
+// two are bit-identical.
+// ---------------------------------------------------------------------------
+template <int MR, int NR>
+__global__ __launch_bounds__(256, 2) void conv1x1_direct_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int BC = 16 * MR;
+  constexpr int W_BYTES = BC * 64;  // one 32-channel chunk of the block's weights
+  constexpr int WJ = BC / 16;       // its DMA instructions (16 rows x 64 B each)
+  constexpr int MAXW = (WJ + 3) / 4;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int col = lane & 15, quad = lane >> 4;
+  const int cout0 = blockIdx.y * BC;
+  const int wcout_pad = (a.Cout + 15) & ~15;
+  const int cin_pad = (a.Cin + 31) & ~31;
+  const int nch = cin_pad >> 5;
+  const int HW = a.Ho * a.Wo;
+  const int npix = a.B * HW;
+  const int ntiles = (npix + 64 * NR - 1) / (64 * NR);
+  for (int c = 0; c < nch; ++c) {
+#pragma unroll
+    for (int it = 0; it < MAXW; ++it) {
+      const int j = wave + 4 * it;
+      if (j < WJ) {
+        const int row = j * 16 + (lane >> 2);
+        const int q = (lane & 3) ^ swz(row);
+        const int co = cout0 + row;
+        const void* src = co < wcout_pad ? (const void*)(a.w + (size_t)co * cin_pad + q * 8 + c * 32)
+                                         : (const void*)g_zero16;
+        __builtin_amdgcn_global_load_lds(src, (void*)(smem + c * W_BYTES + j * 1024), 16, 0, 0);
+      }
+    }
+  }
+  __syncthreads();
+  f32x4 bias[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    const int co = cout0 + m * 16 + quad * 4;  // bias is padded to Cout_pad16
+    bias[m] = co < wcout_pad ? *(const f32x4*)(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // per-lane A fragment offsets within a chunk
+  int aoff[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    const int row = m * 16 + col;
+    aoff[m] = row * 64 + ((quad ^ swz(row)) << 4);
+  }
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const bf16_t* src[NR];
+    bool pv[NR];
+    int pb[NR], py[NR], px[NR];
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      const int p = t * 64 * NR + wave * 16 * NR + n * 16 + col;
+      pv[n] = p < npix;
+      const int pp = pv[n] ? p : 0;
+      pb[n] = pp / HW;
+      const int r = pp - pb[n] * HW;
+      py[n] = r / a.Wo;
+      px[n] = r - py[n] * a.Wo;
+      src[n] = a.in + (size_t)pp * a.in_cs + a.in_co + quad * 8;
+    }
+    // unconditional loads (invalid pixels / channels read the zero block):
+    // a branch around a load would make the compiler drain vmcnt to 0 before
+    // the MFMAs, i.e. wait for the prefetched chunk as well
+    auto load = [&](int c, uint4 (&B)[NR]) {
+      const bool kin = c * 32 + quad * 8 < a.Cin;
+#pragma unroll
+      for (int n = 0; n < NR; ++n)
+        B[n] = *(const uint4*)((pv[n] && kin) ? (const void*)(src[n] + c * 32) : (const void*)g_zero16);
+    };
+    f32x4 acc[MR][NR];
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+#pragma unroll
+      for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto mma = [&](int c, const uint4 (&B)[NR]) {
+      const uint8_t* Wl = smem + c * W_BYTES;
+      bf16x8 A[MR];
+#pragma unroll
+      for (int m = 0; m < MR; ++m) A[m] = __builtin_bit_cast(bf16x8, *(const uint4*)(Wl + aoff[m]));
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int n = 0; n < NR; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[m], __builtin_bit_cast(bf16x8, B[n]),
+                                                              acc[m][n], 0, 0, 0);
+    };
+    // ping-pong register buffers, chunk c+1 in flight during chunk c's MFMAs
+    // (indices clamped instead of branched, so the loads stay countable)
+    uint4 B0[NR], B1[NR];
+    load(0, B0);
+    for (int c = 0; c < nch; c += 2) {
+      load(c + 1 < nch ? c + 1 : nch - 1, B1);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs
+      mma(c, B0);
+      __builtin_amdgcn_sched_barrier(0);
+      load(c + 2 < nch ? c + 2 : nch - 1, B0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + 1 < nch) mma(c + 1, B1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias);
+  }
+}
+
 // Input-channel chunks (32 channels) of the larger group.
 static int conv_nch(const ConvArgs& a) {
   int cin = a.Cin;
@@ -711,6 +829,57 @@ static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, int
   return launch_status("conv_patch");
 }
 
+// 1x1 direct kernel: LDS = the block's resident weights
+static size_t direct_smem(const ConvArgs& a, int MR) {
+  return (size_t)((a.Cin + 31) / 32) * 16 * MR * 64;
+}
+
+template <int MR, int NR>
+static int launch_direct_t(const ConvArgs& a, int persist, hipStream_t s) {
+  static bool attr = false;
+  auto fn = conv1x1_direct_kernel<MR, NR>;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      set_error("hipFuncSetAttribute: %s", hipGetErrorString(e));
+      return -(int)e;
+    }
+    attr = true;
+  }
+  const size_t smem = direct_smem(a, MR);
+  static size_t occ_smem[16] = {0};
+  static int occ_val[16] = {0};
+  int occ = 0;
+  for (int i = 0; i < 16; ++i)
+    if (occ_smem[i] == smem) occ = occ_val[i];
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, smem) != hipSuccess || occ < 1)
+      occ = 1;
+    (void)hipGetLastError();
+    for (int i = 0; i < 16; ++i)
+      if (occ_smem[i] == 0) {
+        occ_smem[i] = smem;
+        occ_val[i] = occ;
+        break;
+      }
+  }
+  const int ytiles = ceil_div((a.Cout + 15) / 16, MR);
+  const int ntiles = ceil_div(a.B * a.Ho * a.Wo, 64 * NR);
+  int gx = ntiles;
+  if (persist) gx = std::min(ntiles, std::max(1, num_cus() * occ / ytiles));
+  fn<<<dim3(gx, ytiles), 256, smem, s>>>(a);
+  return launch_status("conv1x1_direct");
+}
+
+static bool direct_ok(const ConvArgs& a, const ConvCfg& c) {
+  const int T = (a.Cout + 15) / 16;
+  return a.k == 1 && a.stride == 1 && a.pad == 0 && a.g2_cout0 <= 0 && a.Hin == a.Ho &&
+         a.Win == a.Wo && (c.mr <= T || c.mr == 1) && a.in_cs % 8 == 0 && a.in_co % 8 == 0 &&
+         direct_smem(a, c.mr) <= 160 * 1024;
+}
+
 // stride-2 patches are ~4x the tile: only tiles whose offset registers and
 // accumulators fit without spills (NR <= 2, MR * NR <= 8) are built for S = 2
 template <int MR, int NR>
@@ -742,6 +911,8 @@ static const int kTiles[][2] = {{8, 2}, {8, 1}, {5, 2}, {5, 1}, {4, 4}, {4, 2}, 
                                 {2, 4}, {2, 2}, {2, 1}, {1, 4}, {1, 2}, {1, 1}};
 
 bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c) {
+  if (c.kind == 1) return direct_ok(a, c);
+  if (c.kind != 0) return false;
   const int T = (a.Cout + 15) / 16;
   if (c.mr > T && c.mr > 1) return false;
   if (a.stride == 2 && (c.nr > 2 || c.mr * c.nr > 8 || a.k != 3)) return false;  // patch_s2_ok
@@ -755,15 +926,16 @@ bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c) {
 int launch_conv_cfg(const ConvArgs& a, const ConvCfg& c, hipStream_t s) {
   PatchGeo g;
   size_t sm;
-  if (!conv_cfg_ok(a, c) || !patch_geo(a, c, g, sm)) {
+  if (!conv_cfg_ok(a, c) || (c.kind == 0 && !patch_geo(a, c, g, sm))) {
     set_error("conv config MR=%d NR=%d G=%d resw=%d not valid for this layer", c.mr, c.nr, c.G,
               c.resw);
     return RV_EINVAL;
   }
 #define RV_PATCH(M_, N_)                                                                     \
   if (c.mr == M_ && c.nr == N_)                                                              \
-    return c.resw ? launch_patch_ks<M_, N_, true>(a, g, sm, c.persist, s)                    \
-                  : launch_patch_ks<M_, N_, false>(a, g, sm, c.persist, s);
+    return c.kind == 1 ? launch_direct_t<M_, N_>(a, c.persist, s)                            \
+           : c.resw    ? launch_patch_ks<M_, N_, true>(a, g, sm, c.persist, s)               \
+                       : launch_patch_ks<M_, N_, false>(a, g, sm, c.persist, s);
   RV_PATCH(8, 2) RV_PATCH(8, 1) RV_PATCH(5, 2) RV_PATCH(5, 1) RV_PATCH(4, 4) RV_PATCH(4, 2)
   RV_PATCH(4, 1) RV_PATCH(2, 4) RV_PATCH(2, 2) RV_PATCH(2, 1) RV_PATCH(1, 4) RV_PATCH(1, 2)
   RV_PATCH(1, 1)
@@ -793,6 +965,14 @@ int conv_candidates(const ConvArgs& a, ConvCfg* out, int cap) {
           if (n < cap) out[n] = ConvCfg{t[0], t[1], 1, resw, persist};
           ++n;
         }
+      }
+    }
+    // 1x1 layers: the direct-B kernel
+    for (int persist = 1; persist >= 0; --persist) {
+      const ConvCfg d{t[0], t[1], 1, 1, persist, 1};
+      if (direct_ok(a, d)) {
+        if (n < cap) out[n] = d;
+        ++n;
       }
     }
   }

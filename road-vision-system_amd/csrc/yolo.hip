@@ -947,9 +947,9 @@ extern "C" int rv_yolo_autotune(void* h, const uint8_t* lb, int B, void* ws, siz
     }
     if (dbg)
       fprintf(stderr, "[autotune] launch %2zu %3dx%-3d k%d s%d %4d->%-4d default %7.1f us best %7.1f us"
-                      " MR=%d NR=%d G=%d resw=%d (%d cfgs)\n",
+                      " MR=%d NR=%d G=%d resw=%d persist=%d kind=%d (%d cfgs)\n",
               i, a.Ho, a.Wo, a.k, a.stride, a.Cin, a.Cout, t0 * 1e3, tbest * 1e3, best[i].mr,
-              best[i].nr, best[i].G, best[i].resw, n);
+              best[i].nr, best[i].G, best[i].resw, best[i].persist, best[i].kind, n);
   }
   hipEventDestroy(e0);
   hipEventDestroy(e1);
@@ -960,18 +960,19 @@ extern "C" int rv_yolo_autotune(void* h, const uint8_t* lb, int B, void* ws, siz
   return st;
 }
 
-// The autotuned configuration of conv launch `idx` (cfg5 = {MR, NR, G, resw,
-// persist}; MR = 0: the default heuristic).  Returns the number of launches.
-extern "C" int rv_yolo_tuned_config(void* h, int idx, int* cfg5) {
+// The autotuned configuration of conv launch `idx` (cfg6 = {MR, NR, G, resw,
+// persist, kind}; MR = 0: the default heuristic).  Returns the number of launches.
+extern "C" int rv_yolo_tuned_config(void* h, int idx, int* cfg6) {
   if (!h) return RV_EINVAL;
   Model* M = (Model*)h;
-  if (cfg5 && idx >= 0 && idx < (int)M->tuned.size()) {
+  if (cfg6 && idx >= 0 && idx < (int)M->tuned.size()) {
     const ConvCfg& c = M->tuned[idx];
-    cfg5[0] = c.mr;
-    cfg5[1] = c.nr;
-    cfg5[2] = c.G;
-    cfg5[3] = c.resw;
-    cfg5[4] = c.persist;
+    cfg6[0] = c.mr;
+    cfg6[1] = c.nr;
+    cfg6[2] = c.G;
+    cfg6[3] = c.resw;
+    cfg6[4] = c.persist;
+    cfg6[5] = c.kind;
   }
   return (int)M->tuned.size();
 }

@@ -136,12 +136,12 @@ class YoloEngine:
         return bad.value
 
     def tuned_configs(self):
-        """[(MR, NR, G, resw, persist)] per conv launch ([] before autotune)."""
+        """[(MR, NR, G, resw, persist, kind)] per conv launch ([] before autotune)."""
         lib = _lib.load()
         n = lib.rv_yolo_tuned_config(self._h, -1, None)
         out = []
         for i in range(max(n, 0)):
-            c = (ctypes.c_int * 5)()
+            c = (ctypes.c_int * 6)()
             lib.rv_yolo_tuned_config(self._h, i, c)
             out.append(tuple(c))
         return out
