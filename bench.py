@@ -182,12 +182,12 @@ def main():
     t_hbm = conv_bytes_per_step / (PEAK_HBM * 1e9)
     t_mfma = conv_flop_per_step / (PEAK_BF16 * 1e12)
 
-    # HBM bytes of the conv_patch launches of one step, from the committed
+    # HBM bytes of the conv launches of one step, from the committed
     # PMC passes of this configuration (tools/gpu_pmc.sh -> pmc_traffic.json)
     traffic = None
     tp = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
     if os.path.exists(tp):
-        traffic = json.load(open(tp)).get("conv_patch_bytes_per_step")
+        traffic = json.load(open(tp)).get("conv_bytes_per_step")
     total_frames = world * S * K
     value = total_frames / elapsed
     res = {
@@ -215,15 +215,15 @@ def main():
                                  f"graphs, {args.depth}-stage software pipeline over steps "
                                  "(preprocess / YOLO / NMS+SORT of consecutive steps overlap)")},
         "roofline": {
-            "kernel": "conv_patch (all YOLOv8n conv launches of a step, HIP events on the launch "
-                      "stream)",
+            "kernel": "conv family: conv_patch_kernel + conv1x1_direct_kernel (all YOLOv8n conv "
+                      "launches of a step, HIP events on the launch stream)",
             "bound": "hbm" if t_hbm >= t_mfma else "mfma",
             "achieved": round(achieved_bw if t_hbm >= t_mfma else achieved, 2),
             "peak": PEAK_HBM if t_hbm >= t_mfma else PEAK_BF16,
             "unit": "GB/s" if t_hbm >= t_mfma else "TFLOP/s",
             "frac": round(achieved_bw / PEAK_HBM if t_hbm >= t_mfma else achieved / PEAK_BF16, 5),
             "traffic": traffic,
-            "traffic_unit": "bytes per step (all conv_patch launches; rocprofv3 PMC FETCH_SIZE x2 "
+            "traffic_unit": "bytes per step (all conv launches; rocprofv3 PMC FETCH_SIZE x2 "
                             "+ WRITE_SIZE, profiles/r01/pmc_traffic.json)",
             "algorithmic_bytes_per_step": round(conv_bytes_per_step),
             "algorithmic_gflop_per_step": round(conv_flop_per_step / 1e9, 2),

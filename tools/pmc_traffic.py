@@ -1,4 +1,5 @@
-"""HBM traffic of the conv_patch launches of one bench step from the PMC
+"""HBM traffic of the conv launches (conv_patch_kernel + conv1x1_direct_kernel)
+of one bench step from the PMC
 passes of tools/gpu_pmc.sh (FETCH_SIZE / WRITE_SIZE, KB): per the gfx950
 calibration in MI355X_MICROARCH.md, FETCH_SIZE counts half the bytes of a
 wide streaming read (x2), WRITE_SIZE counts 16-B-per-lane stores exactly.
@@ -10,6 +11,8 @@ import sys
 
 sys.path[:0] = [os.path.dirname(os.path.abspath(__file__))]
 from pmc_report import load  # noqa: E402
+
+CONV_KERNELS = ("conv_patch_kernel", "conv1x1_direct_kernel")
 
 
 def main():
@@ -29,11 +32,11 @@ def main():
         k[0] += 1
         k[1] += rd
         k[2] += wr
-        if name.startswith("conv_patch_kernel"):
+        if name.startswith(CONV_KERNELS):
             fetch += rd
             write += wr
-    res = {"conv_patch_bytes_per_step": fetch + write, "conv_patch_read_bytes": fetch,
-           "conv_patch_write_bytes": write,
+    res = {"conv_bytes_per_step": fetch + write, "conv_read_bytes": fetch,
+           "conv_write_bytes": write, "conv_kernels": list(CONV_KERNELS),
            "per_kernel": {k: {"launches": c, "read_bytes": r, "write_bytes": w}
                           for k, (c, r, w) in per_kernel.items()},
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over one eager bench step "
