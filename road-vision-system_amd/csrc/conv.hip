@@ -367,14 +367,21 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[MR][NR]
 // disjoint 4-bank groups.  The swizzle depends on the column only, so a
 // kernel-row step (ky) moves every address by the same PW * 64 and the
 // per-lane tap addresses are precomputed once per block (NR x K values).
-// Stride-2 convs (fragment pixels two columns apart) use an 80-B stride
-// instead (4 quarters + a pad slot from the zero block): 16 pixels 40 dwords
-// apart are again disjoint, with no swizzle.  The DMA stays lane-linear:
-// lane l of DMA instruction j fills slot L = 64 j + l, i.e. pixel L / SL,
-// slot quarter L % SL (SL = 4 or 5 slots per pixel).
+// Stride-2 convs store the patch columns de-interleaved (even columns, then
+// odd ones: stored column sc of column px = px/2 or HE + px/2, HE = the even
+// count), so the 16 output pixels of a fragment -- patch columns two apart --
+// read 16 consecutive stored columns at every tap (kx = 0: sc = c, 1: HE + c,
+// 2: c + 1) and the same swizzle, on the stored column, keeps them
+// conflict-free.  The DMA stays lane-linear: lane l of DMA instruction j
+// fills slot L = 64 j + l, i.e. stored pixel L / 4, slot quarter L % 4.
 template <int S>
 constexpr int patch_pixb() {
-  return S == 1 ? 64 : 80;
+  return 64;
+}
+// stored column of patch column px (S = 2: de-interleaved)
+template <int S>
+__device__ __forceinline__ int patch_scol(int px, int PW) {
+  return S == 1 ? px : ((px & 1) ? (PW + 1) / 2 + (px >> 1) : (px >> 1));
 }
 
 // Per-lane DMA source offsets of one patch (elements from the image base,
@@ -457,9 +464,8 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
     const int pr = oin[n] ? orow[n] * S : 0, pc = oin[n] ? ocol[n] * S : 0;
 #pragma unroll
     for (int kx = 0; kx < K; ++kx) {
-      const int pp = pr * g.PW + pc + kx;
-      boff[n][kx] = PB == 64 ? pp * 64 + ((quad ^ (((pc + kx) >> 2) & 3)) << 4)
-                             : pp * PB + quad * 16;
+      const int sc = patch_scol<S>(pc + kx, g.PW);
+      boff[n][kx] = (pr * g.PW + sc) * 64 + ((quad ^ ((sc >> 2) & 3)) << 4);
     }
   }
   f32x4 bias[MR];
@@ -483,10 +489,12 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
       const int L = 64 * (wave + 4 * it) + lane;
       const int pix = L / SL, q = L - SL * pix;
       const int py = (int)(((float)pix + 0.5f) * inv_pw);
-      const int px = pix - py * g.PW;
+      const int sc = pix - py * g.PW;  // stored column
+      const int he = (g.PW + 1) >> 1;
+      const int px = S == 1 ? sc : (sc < he ? 2 * sc : 2 * (sc - he) + 1);
       const int iy = iy0 + py, ix = ix0 + px;
-      const int sq = PB == 64 ? q ^ ((px >> 2) & 3) : q;  // source quarter of slot q
-      const bool ok = sq < 4 && pix < npp && (unsigned)iy < (unsigned)a.Hin &&
+      const int sq = q ^ ((sc >> 2) & 3);  // source quarter of slot q
+      const bool ok = pix < npp && (unsigned)iy < (unsigned)a.Hin &&
                       (unsigned)ix < (unsigned)a.Win;
       poff[it] = ok ? (iy * a.Win + ix) * a.in_cs + sq * 8 : -1;
       if ((nch - 1) * 32 + sq * 8 >= Cin) tailbad |= 1u << it;
@@ -757,7 +765,7 @@ static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& 
   if (g.R < 1) return false;
   g.PH = (g.R - 1) * a.stride + a.k;
   g.PW = (g.C - 1) * a.stride + a.k;
-  g.pinst = ceil_div(g.PH * g.PW * (a.stride == 1 ? 4 : 5), 64);  // 16-B slots (patch_pixb)
+  g.pinst = ceil_div(g.PH * g.PW * 4, 64);  // 4 16-B slots per pixel (patch_pixb)
   g.p_bytes = g.pinst * 1024;
   g.tiles_x = ceil_div(a.Wo, g.C);
   g.tiles_y = ceil_div(a.Ho, g.R);
