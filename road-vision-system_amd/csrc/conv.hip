@@ -1230,9 +1230,9 @@ int launch_conv0(const uint8_t* img, int B, int H, int W, const float* w, const 
 constexpr int kStR = 8, kStC = 32;                      // X1 tile
 constexpr int kStXR = 2 * kStR + 1, kStXC = 2 * kStC + 2;  // X0 tile (17 x 66)
 constexpr int kStLR = 2 * kStXR + 1, kStLC = 2 * kStXC + 1;  // lb tile (35 x 133 px)
-constexpr int kStLS = kStLC * 3 + 5;                    // lb row stride (u16), 404
+constexpr int kStLS = kStLC * 3 + 5;                    // lb row stride (bytes), 404
 constexpr int kStXB = kStXR * kStXC * 32;               // X0 tile bytes (35,904)
-constexpr int kStLB = kStLR * kStLS * 2;                // lb tile bytes (28,280)
+constexpr int kStLB = kStLR * kStLS;                    // lb tile bytes (14,140)
 
 __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ img, int B, int H,
                                                    int W, const float* __restrict__ w0,
@@ -1242,7 +1242,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
                                                    uint16_t* __restrict__ out, int out_cs) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* xs = smem;                               // X0 tile: [17][66] px x 32 B
-  uint16_t* ls = (uint16_t*)(smem + kStXB);         // lb tile: [35][404] u16
+  uint8_t* ls = smem + kStXB;                       // lb tile: [35][404] u8
   const int H0 = (H + 1) / 2, W0 = (W + 1) / 2;     // X0 map
   const int H1 = (H0 + 1) / 2, W1 = (W0 + 1) / 2;   // X1 map
   const int tiles_x = (W1 + kStC - 1) / kStC, tiles_y = (H1 + kStR - 1) / kStR;
@@ -1258,7 +1258,8 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
 
-  // ---- 1. letterbox tile -> LDS as bf16 bit patterns (0 outside the image)
+  // ---- 1. letterbox tile -> LDS as u8 (0 outside the image); the bf16 bit
+  //      patterns of the (exact) byte values are formed when gathered
   {
     constexpr int kDw = (kStLC * 3 + 1 + 3) / 4;       // dwords per row (covers 399 B + 1)
     constexpr int kN = kStLR * kDw;
@@ -1290,13 +1291,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
         const int i = i0 + u * 256;
         if (i < kN) {
           const int r = i / kDw, d = i - (i / kDw) * kDw;
-          const uint32_t f0 = __float_as_uint((float)(dv[u] & 255));
-          const uint32_t f1 = __float_as_uint((float)((dv[u] >> 8) & 255));
-          const uint32_t f2 = __float_as_uint((float)((dv[u] >> 16) & 255));
-          const uint32_t f3 = __float_as_uint((float)(dv[u] >> 24));
-          uint32_t* dst = (uint32_t*)(ls + r * kStLS + 4 * d);  // element e = byte column e - 1
-          dst[0] = (f0 >> 16) | (f1 & 0xFFFF0000u);
-          dst[1] = (f2 >> 16) | (f3 & 0xFFFF0000u);
+          *(uint32_t*)(ls + r * kStLS + 4 * d) = dv[u];  // element e = byte column e - 1
         }
       }
     }
@@ -1342,7 +1337,8 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
     const int base = 2 * yr * kStLS + 2 * xr * 3;
     bf16x8 X;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) X[j] = __builtin_bit_cast(__bf16, ls[base + koff[j]]);
+    for (int j = 0; j < 8; ++j)
+      X[j] = __builtin_bit_cast(__bf16, (uint16_t)(__float_as_uint((float)ls[base + koff[j]]) >> 16));
     f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, X, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, X, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, X, acc, 0, 0, 0);
