@@ -88,7 +88,7 @@ def main():
     ap.add_argument("--eager", action="store_true", help="launch kernels eagerly (no HIP graph)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip the per-layer conv kernel autotuning before the timed region")
-    ap.add_argument("--depth", type=int, default=int(os.environ.get("RV_PIPE_DEPTH", 2)),
+    ap.add_argument("--depth", type=int, default=int(os.environ.get("RV_PIPE_DEPTH", 3)),
                     help="pipelined steps: 3 = Y(k) || P(k+1) || T(k-1), 2 = [T(k-1) || P(k)] -> Y(k)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one graph per step; no overlap of step k's NMS+SORT with step k+1")

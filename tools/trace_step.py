@@ -25,7 +25,8 @@ for f in range(2):
 if not os.environ.get("NO_TUNE"):
     eng.autotune(frames[0])
 torch.cuda.synchronize()
-run = OverlappedSteps(eng, [frames[2 + k] for k in range(N)], [ts[2 + k] for k in range(N)])
+run = OverlappedSteps(eng, [frames[2 + k] for k in range(N)], [ts[2 + k] for k in range(N)],
+                      depth=int(os.environ.get("RV_PIPE_DEPTH", 3)))
 torch.cuda.synchronize()
 time.sleep(0.05)
 t = time.perf_counter()
