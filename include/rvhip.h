@@ -191,11 +191,14 @@ size_t rv_nms_smem_bytes(void);
  * python gain), pad_x, pad_y, clip_w, clip_h}; keep_mask4 (nullable = keep
  * all): 128-bit class mask (classes_keep); out: B x max_det x 6
  * {x1,y1,x2,y2,conf,cls} in score order, out_n[B]; cand_total (nullable):
- * candidates per image. */
+ * candidates per image; ws: rv_nms_ws_bytes(B) bytes of device workspace. */
 int rv_nms_postprocess(const void* cand, const int* seg_n, int B, int cap, int nseg,
                        float iou, int max_det, float max_wh, const float* scale5,
                        const uint32_t* keep_mask4, float* out, int* out_n, int* cand_total,
-                       void* stream);
+                       void* ws, size_t ws_bytes, void* stream);
+/* Device workspace rv_nms_postprocess needs for B images (sort keys of
+ * images with more than 4096 candidates). */
+size_t rv_nms_ws_bytes(int B);
 /* Segments of 64 anchors for a raw prediction with A anchors. */
 int rv_cand_segments(int A);
 /* Candidate rows from a reference-layout raw prediction (B, 4+nc, A), in the

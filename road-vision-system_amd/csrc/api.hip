@@ -13,5 +13,5 @@ void set_error(const char* fmt, ...) {
 }
 }  // namespace rv
 
-extern "C" int rv_abi_version(void) { return 1; }
+extern "C" int rv_abi_version(void) { return 2; }
 extern "C" const char* rv_last_error(void) { return rv::g_err; }

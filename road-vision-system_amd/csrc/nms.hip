@@ -12,6 +12,12 @@
 //
 // Sort: 64-bit keys (~score_bits, anchor, slot) bitonic-sorted in LDS
 // (score desc, anchor asc == the stable order of rows in anchor order).
+// Two passes with the same code: nms_kernel<kSortSmall> sorts up to 4096
+// candidates in ~41 KB of LDS (so conv blocks still fit beside it when the
+// track stage overlaps the next forward); an image with more candidates is
+// flagged (out_n = -1) and redone by nms_kernel<kSortCap>, which keeps its
+// keys in the caller's workspace (global memory, ~10 KB of LDS) and whose
+// blocks exit at once for every unflagged image.
 // Greedy: wave 0 walks the sorted list in chunks of 64; each lane tests its
 // candidate against every kept box, builds the 64-bit mask of later chunk
 // members it would suppress, and a uniform scalar loop resolves the chunk.
@@ -20,6 +26,7 @@
 namespace rv {
 
 constexpr int kSortCap = 16384;  // candidates per image held in LDS (128 KB)
+constexpr int kSortSmall = 4096;  // first pass (32 KB of keys)
 constexpr int kMaxDet = 1024;
 constexpr int kMaxSeg = 1024;    // 64-candidate segments per image (<= 65536 slots)
 
@@ -51,29 +58,40 @@ __device__ __forceinline__ bool suppresses(float4 bi, float ai, float4 bj, float
   return (double)ovr > thr;
 }
 
+// LDS bytes of nms_kernel<CAP> for max_det kept boxes (the segment prefix
+// region is padded to 16 B so the float4 arrays after it stay aligned)
+constexpr int kSegBytes = ((kMaxSeg + 1) * 4 + 15) & ~15;
+static size_t nms_smem(int cap_keys, int max_det) {
+  const size_t lds_keys = cap_keys > kSortSmall ? 0 : (size_t)cap_keys * 8;  // overflow: global
+  return lds_keys + kSegBytes + 64 * (16 + 4 + 8) + (size_t)max_det * (16 + 4 + 4);
+}
+
+template <int CAP>
 __global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand,
                                                    const int* __restrict__ seg_n, int nseg, int cap,
                                                    float max_wh, double iou, int max_det,
                                                    ScaleArgs sc, const uint32_t* __restrict__ keep4,
                                                    float* __restrict__ out, int* __restrict__ out_n,
-                                                   int* __restrict__ cand_total) {
+                                                   int* __restrict__ cand_total,
+                                                   uint64_t* __restrict__ gkeys) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint64_t* keys = (uint64_t*)smem;                       // kSortCap
-  float4* kbox = (float4*)(smem + kSortCap * 8);          // kept offset boxes (kMaxDet)
-  float* karea = (float*)(kbox + kMaxDet);                // kMaxDet
-  int* kslot = (int*)(karea + kMaxDet);                   // kMaxDet
-  float4* cbox = (float4*)(kslot + kMaxDet);              // chunk boxes (64)
-  float* carea = (float*)(cbox + 64);                     // 64
-  uint64_t* cmask = (uint64_t*)(carea + 64);              // 64
-  __shared__ int s_nkeep;
-  __shared__ int wsum[16];
-  // exclusive prefix of the segment counts (+ total at [kMaxSeg]); aliases
-  // the kept-box array, which is only used after the sort
-  int* segoff = (int*)kbox;
-  static_assert((kMaxSeg + 1) * 4 <= kMaxDet * 16, "segoff alias");
-
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
+  // overflow pass: only the images the first pass flagged
+  constexpr bool kGlobal = CAP > kSortSmall;
+  if (kGlobal && out_n[b] != -1) return;
+  constexpr size_t kLdsKeys = kGlobal ? 0 : (size_t)CAP * 8;
+  uint64_t* keys = kGlobal ? gkeys + (size_t)b * CAP : (uint64_t*)smem;  // CAP
+  int* segoff = (int*)(smem + kLdsKeys);                  // kMaxSeg + 1: exclusive prefix + total
+  uint64_t* cmask = (uint64_t*)(smem + kLdsKeys + kSegBytes);  // 64
+  float4* cbox = (float4*)(cmask + 64);                   // chunk boxes (64)
+  float* carea = (float*)(cbox + 64);                     // 64
+  float4* kbox = (float4*)(carea + 64);                   // kept offset boxes (max_det)
+  float* karea = (float*)(kbox + max_det);                // max_det
+  int* kslot = (int*)(karea + max_det);                   // max_det
+  __shared__ int s_nkeep;
+  __shared__ int wsum[16];
+
   const Cand* cb = cand + (size_t)b * cap;
   // segment counts -> exclusive prefix (one segment per thread, nseg <= 1024)
   int cnt = 0;
@@ -97,7 +115,11 @@ __global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand
   __syncthreads();
   int n = segoff[kMaxSeg];
   if (cand_total && tid == 0) cand_total[b] = n;
-  if (n > kSortCap) n = kSortCap;  // capacity limit (documented in DESIGN.md)
+  if (CAP == kSortSmall && n > CAP) {  // redone by the overflow pass
+    if (tid == 0) out_n[b] = -1;
+    return;
+  }
+  if (n > CAP) n = CAP;  // capacity limit (documented in DESIGN.md)
   int np2 = 1;
   while (np2 < n) np2 <<= 1;
   for (int i = tid; i < np2; i += blockDim.x) keys[i] = ~0ull;
@@ -261,19 +283,23 @@ __global__ __launch_bounds__(64) void raw_candidates_kernel(const float* __restr
 
 using namespace rv;
 
-extern "C" size_t rv_nms_smem_bytes(void) {
-  return (size_t)kSortCap * 8 + (size_t)kMaxDet * (16 + 4 + 4) + 64 * (16 + 4 + 8);
-}
+// LDS of the first pass at the largest max_det (the overflow pass needs less)
+extern "C" size_t rv_nms_smem_bytes(void) { return nms_smem(kSortSmall, kMaxDet); }
+
+// Workspace of rv_nms_postprocess: the overflow pass's sort keys.
+extern "C" size_t rv_nms_ws_bytes(int B) { return (size_t)(B > 0 ? B : 0) * kSortCap * 8; }
 
 extern "C" int rv_nms_postprocess(const void* cand, const int* seg_n, int B, int cap, int nseg,
                                   float iou, int max_det, float max_wh, const float* scale5,
                                   const uint32_t* keep_mask4, float* out, int* out_n,
-                                  int* cand_total, void* stream) {
+                                  int* cand_total, void* ws, size_t ws_bytes, void* stream) {
   RV_CHECK_ARG(cand && seg_n && out && out_n && scale5, "null pointer");
   RV_CHECK_ARG(B >= 0 && cap > 0 && cap <= 65536, "cap %d outside (0, 65536]", cap);
   RV_CHECK_ARG(nseg > 0 && nseg <= kMaxSeg && nseg * 64 <= cap,
                "nseg %d: need 0 < nseg <= %d and nseg * 64 <= cap %d", nseg, kMaxSeg, cap);
   RV_CHECK_ARG(max_det > 0 && max_det <= kMaxDet, "max_det %d outside (0, %d]", max_det, kMaxDet);
+  RV_CHECK_ARG(ws && ws_bytes >= rv_nms_ws_bytes(B), "workspace %zu B < rv_nms_ws_bytes(%d) = %zu",
+               ws_bytes, B, rv_nms_ws_bytes(B));
   if (B == 0) return RV_OK;
   ScaleArgs sc;
   sc.gain = scale5[0];
@@ -281,22 +307,31 @@ extern "C" int rv_nms_postprocess(const void* cand, const int* seg_n, int B, int
   sc.pad_y = scale5[2];
   sc.clip_w = scale5[3];
   sc.clip_h = scale5[4];
-  const size_t smem = rv_nms_smem_bytes();
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)nms_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipError_t e = hipFuncSetAttribute((const void*)nms_kernel<kSortCap>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)rv_nms_smem_bytes());
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)nms_kernel<kSortSmall>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)nms_smem(kSortSmall, kMaxDet));
     if (e != hipSuccess) {
-      set_error("hipFuncSetAttribute(%zu B LDS): %s", smem, hipGetErrorString(e));
+      set_error("hipFuncSetAttribute(NMS LDS): %s", hipGetErrorString(e));
       (void)hipGetLastError();
       return -(int)e;
     }
     attr = true;
   }
-  nms_kernel<<<B, 1024, smem, as_stream(stream)>>>((const Cand*)cand, seg_n, nseg, cap, max_wh,
-                                                    (double)iou, max_det, sc, keep_mask4, out,
-                                                    out_n, cand_total);
-  return launch_status("rv_nms_postprocess");
+  nms_kernel<kSortSmall><<<B, 1024, nms_smem(kSortSmall, max_det), as_stream(stream)>>>(
+      (const Cand*)cand, seg_n, nseg, cap, max_wh, (double)iou, max_det, sc, keep_mask4, out,
+      out_n, cand_total, nullptr);
+  int st = launch_status("rv_nms_postprocess");
+  if (st) return st;
+  nms_kernel<kSortCap><<<B, 1024, nms_smem(kSortCap, max_det), as_stream(stream)>>>(
+      (const Cand*)cand, seg_n, nseg, cap, max_wh, (double)iou, max_det, sc, keep_mask4, out,
+      out_n, cand_total, (uint64_t*)ws);
+  return launch_status("rv_nms_postprocess (overflow pass)");
 }
 
 extern "C" int rv_cand_segments(int A) { return A > 0 ? ceil_div(A, 64) : 0; }

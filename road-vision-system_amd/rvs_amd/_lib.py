@@ -71,7 +71,8 @@ _SIGS = {
     "rv_nms_smem_bytes": (c_size_t, []),
     "rv_nms_postprocess": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int,
                                    c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                   c_void_p]),
+                                   c_void_p, c_size_t, c_void_p]),
+    "rv_nms_ws_bytes": (c_size_t, [c_int]),
     "rv_cand_segments": (c_int, [c_int]),
     "rv_yolo_cand_segments": (c_int, [c_void_p]),
     "rv_candidates_from_raw": (c_int, [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int,

@@ -87,6 +87,9 @@ class YoloEngine:
         self.seg_n = torch.zeros((2, self.max_batch, max(self.nseg, lib.rv_cand_segments(self.A))),
                                  dtype=torch.int32, device=dev)
         self.cand_n = torch.zeros(self.max_batch, dtype=torch.int32, device=dev)  # set by NMS
+        # NMS workspace (sort keys of images with more than 4096 candidates)
+        self.nms_ws = torch.empty(max(int(_lib.load().rv_nms_ws_bytes(self.max_batch)), 8),
+                                  dtype=torch.uint8, device=dev)
         self._nseg_cur = self.nseg
         self.dets = torch.zeros((self.max_batch, self.max_det, 6), dtype=torch.float32, device=dev)
         self.det_n = torch.zeros(self.max_batch, dtype=torch.int32, device=dev)
@@ -150,7 +153,8 @@ class YoloEngine:
         """NMS + scale_boxes + class filter of candidate slot `slot`."""
         call("rv_nms_postprocess", ptr(self.cand[slot]), ptr(self.seg_n[slot]), B, self.cap,
              self._nseg_cur, self.iou, self.max_det, self.max_wh, ptr(self.scale5), ptr(self.keep),
-             ptr(self.dets), ptr(self.det_n), ptr(self.cand_n), stream_ptr())
+             ptr(self.dets), ptr(self.det_n), ptr(self.cand_n), ptr(self.nms_ws),
+             self.nms_ws.numel(), stream_ptr())
         return self.dets[:B], self.det_n[:B]
 
     def nms_from_raw(self, raw: torch.Tensor):

@@ -95,7 +95,9 @@ def _raw_from_boxes(boxes, scores, cls, A, nc=80):
     return raw
 
 
-@pytest.mark.parametrize("case", ["ties", "dense", "empty", "many", "maxdet", "classes"])
+# "overflow": more candidates than the first NMS pass sorts in LDS (4096), so
+# the image is redone by the 16384-key overflow pass
+@pytest.mark.parametrize("case", ["ties", "dense", "empty", "many", "overflow", "maxdet", "classes"])
 def test_nms_edge_cases(cuda, case):
     rng = np.random.default_rng(hash(case) % 2**32)
     A = 5040
@@ -104,7 +106,8 @@ def test_nms_edge_cases(cuda, case):
     if case == "empty":
         boxes, scores, cls = np.zeros((0, 4)), np.zeros(0), np.zeros(0, int)
     else:
-        n = {"ties": 300, "dense": 400, "many": 4000, "maxdet": 200, "classes": 500}[case]
+        n = {"ties": 300, "dense": 400, "many": 4000, "overflow": 5000, "maxdet": 200,
+             "classes": 500}[case]
         xy = rng.uniform(0, 600, (n, 2))
         wh = rng.uniform(10, 120, (n, 2)) if case != "dense" else rng.uniform(200, 260, (n, 2))
         boxes = np.concatenate([xy, xy + wh], 1)
