@@ -230,6 +230,32 @@ int rv_sort_update(void* state_in, void* state_out, int S, int tmax, const float
 int rv_sort_export(const void* state, int S, int tmax, double* x_out, int* meta, int* T_out,
                    void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* Augment: fog + rain synthetic inputs (EnhancedFogSynthesizer.synthesize,  */
+/* src/augment/fog.py:239-299; tools/fog_batch.py:7-34 drives it offline).   */
+/* Restated subset: depth proxy, value-noise beta map, transmission, airlight */
+/* gradient map, scattering I = J t + A (1 - t), global veil, tint, gamma,    */
+/* plus rain streaks.  Parameters are drawn on the host                       */
+/* (rvs_amd/augment/fog.py); the OpenCV filters are not restated. */
+/* ------------------------------------------------------------------------ */
+#define RV_FOG_NCONST 26
+#define RV_FOG_NPARAM 16
+/* consts (host, RV_FOG_NCONST f32): {vx, vy, dv_max, d_min, d_range, 0,
+ *   rain_p, rain_len, n_oct, [gh, gw, amp, 0] x 4 octaves, norm}.
+ * scene (device f32, 4*H + W): per-row 0.7*dp/dp_max, depth factor
+ *   (sky boost x road damp), global-veil weight, airlight vertical gradient;
+ *   then the per-column airlight horizontal gradient.
+ * frame_params (device, B x RV_FOG_NPARAM f32): {beta, A_b, A_g, A_r,
+ *   A_scale, tint_b, tint_g, tint_r, gamma, rain_seed (< 2^24), 0...}.
+ * grids (device, B x grid_stride f32): per frame, the octaves' value-noise
+ *   grids, (gh+1) x (gw+1) each, concatenated.
+ * ws: rv_fog_ws_bytes(B) bytes of device scratch (noise min / max). */
+size_t rv_fog_ws_bytes(int B);
+int rv_fog_rain_u8(const uint8_t* in, uint8_t* out, int B, int H, int W, int pitch,
+                   const float* consts, int n_consts, const float* scene,
+                   const float* frame_params, const float* grids, int grid_stride,
+                   void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -44,6 +44,11 @@ _SIGS = {
     "rv_clahe_median_letterbox_fits": (c_int, [c_int, c_int, c_int, c_int, POINTER(c_int)]),
     "rv_gray_span_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                 c_void_p]),
+    # augment
+    "rv_fog_ws_bytes": (c_size_t, [c_int]),
+    "rv_fog_rain_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                               c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_size_t,
+                               c_void_p]),
     "rv_letterbox_geometry": (c_int, [c_int, c_int, c_int, c_int, POINTER(c_int)]),
     "rv_letterbox_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                 POINTER(c_int), c_void_p]),

@@ -86,9 +86,10 @@ def _setup(cuda, H, W, B, variant=0):
     return eng, Introspect(eng, B), specs, params, lb.cpu().numpy(), raw.cpu().numpy()
 
 
-@pytest.mark.parametrize("H,W,B", [(640, 640, 1), (1080, 1920, 2)])
-def test_every_conv_layerwise(cuda, H, W, B):
-    eng, ins, specs, params, lb, raw = _setup(cuda, H, W, B)
+@pytest.mark.parametrize("H,W,B,variant", [(640, 640, 1, 0), (1080, 1920, 2, 0),
+                                            (640, 640, 1, 2)])  # 2 = YOLOv8m (config 5)
+def test_every_conv_layerwise(cuda, H, W, B, variant):
+    eng, ins, specs, params, lb, raw = _setup(cuda, H, W, B, variant)
     assert len(ins.recs) == len(specs) - 1  # all but model.0 go through conv_mfma
     worst = []
     for r in ins.recs:
