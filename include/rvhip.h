@@ -58,6 +58,19 @@ int rv_clahe_ycrcb_u8(const uint8_t* in, uint8_t* out, int B, int H, int W,
                       int pitch, int tiles, double clip, void* ws,
                       size_t ws_bytes, void* stream);
 
+/* CLAHEDehaze space="LAB" (clahe_dehaze.py:21-25): cv2.COLOR_BGR2LAB, CLAHE
+ * on L, cv2.COLOR_LAB2BGR, 8U sRGB / D65 integer paths (OpenCV color_lab.cpp
+ * RGB2Lab_b / Lab2RGBinteger, restated; csrc/lab.h).  Same arguments and
+ * workspace as rv_clahe_ycrcb_u8.  The first LAB call uploads the Lab tables
+ * synchronously; call rv_lab_init() once before capturing it in a graph. */
+int rv_clahe_lab_u8(const uint8_t* in, uint8_t* out, int B, int H, int W,
+                    int pitch, int tiles, double clip, void* ws,
+                    size_t ws_bytes, void* stream);
+int rv_lab_init(void);
+/* Host copy of the Lab tables (parity tests): {u16 gamma[256], cbrt[3072],
+ * yf[512], invg[4096]; i32 cf[9], ci[9]}, exactly 15944 bytes. */
+int rv_lab_tables_host(void* out, size_t bytes);
+
 /* Exact per-channel k x k median with replicated borders (cv2.medianBlur on
  * 8UC3).  k is the already-normalised kernel size (median_derain.py:11-13:
  * odd, clamped to [3, 9]). in and out may not alias. */

@@ -34,6 +34,10 @@ def lib():
         L.oracle_clahe_ycrcb.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_double]
         L.oracle_clahe_u8c1.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_double]
         L.oracle_bgr2ycrcb.argtypes = [c_void_p, c_void_p, c_int]
+        L.oracle_clahe_lab.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_double]
+        L.oracle_bgr2lab.argtypes = [c_void_p, c_void_p, c_int]
+        L.oracle_lab2bgr.argtypes = [c_void_p, c_void_p, c_int]
+        L.oracle_lab_tables.argtypes = [c_void_p]
         L.oracle_ycrcb2bgr.argtypes = [c_void_p, c_void_p, c_int]
         L.oracle_median_u8c3.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int]
         L.oracle_letterbox_geometry.argtypes = [c_int, c_int, c_int, c_int, POINTER(c_int)]
@@ -59,6 +63,39 @@ def clahe_ycrcb(img: np.ndarray, tiles: int = 8, clip: float = 2.0) -> np.ndarra
     out = np.empty_like(img)
     lib().oracle_clahe_ycrcb(_p(img), _p(out), H, W, tiles, clip)
     return out
+
+
+def clahe_lab(img: np.ndarray, tiles: int = 8, clip: float = 2.0) -> np.ndarray:
+    """CLAHEDehaze space='LAB' (clahe_dehaze.py:21-25), see rv_oracle.c."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    H, W, _ = img.shape
+    out = np.empty_like(img)
+    lib().oracle_clahe_lab(_p(img), _p(out), H, W, tiles, clip)
+    return out
+
+
+def bgr2lab(img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    out = np.empty_like(img)
+    lib().oracle_bgr2lab(_p(img), _p(out), img.size // 3)
+    return out
+
+
+def lab2bgr(img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    out = np.empty_like(img)
+    lib().oracle_lab2bgr(_p(img), _p(out), img.size // 3)
+    return out
+
+
+LAB_TABLE_BYTES = 2 * (256 + 3072 + 512 + 4096) + 4 * 18
+
+
+def lab_tables() -> bytes:
+    """The oracle's 8U Lab tables, packed like rv_lab_tables_host()."""
+    buf = np.zeros(LAB_TABLE_BYTES, np.uint8)
+    lib().oracle_lab_tables(_p(buf))
+    return buf.tobytes()
 
 
 def clahe_u8c1(plane: np.ndarray, tiles: int = 8, clip: float = 2.0) -> np.ndarray:

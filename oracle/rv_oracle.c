@@ -396,3 +396,150 @@ int oracle_nms(const float* boxes, const float* scores, int n, double iou_thr, i
   free(area);
   return nk < max_keep ? nk : max_keep;
 }
+
+/* ------------------------------------------------------------------------
+ * CLAHEDehaze LAB path (src/preprocess/ops/clahe_dehaze.py:21-25):
+ * cv2.COLOR_BGR2LAB -> CLAHE on L -> cv2.COLOR_LAB2BGR, 8U, sRGB, D65.
+ * Restates OpenCV 4.x imgproc/src/color_lab.cpp's 8-bit integer paths
+ * (RGB2Lab_b: gamma_shift 3, lab_shift 12, 15-bit cube-root table;
+ * Lab2RGBinteger: 14-bit base, L -> (y, f(y)) table, a/b dividers, 4096-entry
+ * inverse-gamma table).  Tables are computed here in double with
+ * round-half-even (OpenCV builds them with softfloat/softdouble).  UNPINNED
+ * against real OpenCV (absent); pinned by CIE known-answer values in
+ * tests/test_oracle_preprocess.py.
+ * ---------------------------------------------------------------------- */
+typedef struct {
+  uint16_t gamma[256];  /* sRGB -> linear, x 255*8 */
+  uint16_t cbrt[3072];  /* f(t) x 2^15 for t = i / (255*8) */
+  uint16_t yf[512];     /* per L: y x 2^14, f(y) x 2^14 */
+  uint16_t invg[4096];  /* linear (i/4096) -> sRGB u8 */
+  int32_t cf[9];        /* BGR-ordered rows X, Y, Z: M_rgb2xyz / white x 2^12 */
+  int32_t ci[9];        /* rows B, G, R over (X, Y, Z): M_xyz2rgb * white x 2^12 */
+} OracleLab;
+
+static const double kRgb2Xyz[9] = {0.412453, 0.357580, 0.180423, 0.212671, 0.715160,
+                                   0.072169, 0.019334, 0.119193, 0.950227};
+static const double kXyz2Rgb[9] = {3.240479, -1.53715, -0.498535, -0.969256, 1.875991,
+                                   0.041556, 0.055648, -0.204043, 1.057311};
+static const double kD65[3] = {0.950456, 1.0, 1.088754};
+
+void oracle_lab_tables(OracleLab* t) {
+  for (int i = 0; i < 256; ++i) {
+    double x = i / 255.0;
+    double g = x <= 0.04045 ? x / 12.92 : pow((x + 0.055) / 1.055, 2.4);
+    t->gamma[i] = (uint16_t)nearbyint(255.0 * 8.0 * g);
+  }
+  for (int i = 0; i < 3072; ++i) {
+    double x = i / (255.0 * 8.0);
+    double f = x < 216.0 / 24389.0 ? x * (841.0 / 108.0) + 16.0 / 116.0 : cbrt(x);
+    t->cbrt[i] = (uint16_t)nearbyint(32768.0 * f);
+  }
+  const double base = 16384.0;
+  for (int i = 0; i < 256; ++i) {
+    double y, ify;
+    if (i <= 20) {
+      y = nearbyint(i * base * 20.0 * 9.0 / (17.0 * 29.0 * 29.0 * 29.0));
+      ify = nearbyint(base * (16.0 / 116.0 + i * 5.0 / (3.0 * 17.0 * 29.0)));
+    } else {
+      double fy = i * 100.0 * base / (255.0 * 116.0) + 16.0 * base / 116.0;
+      ify = nearbyint(fy);
+      y = nearbyint(fy * fy * fy / (base * base));
+    }
+    t->yf[2 * i] = (uint16_t)y;
+    t->yf[2 * i + 1] = (uint16_t)ify;
+  }
+  for (int i = 0; i < 4096; ++i) {
+    double x = i / 4096.0;
+    double v = x <= 0.0031308 ? 12.92 * x : 1.055 * pow(x, 1.0 / 2.4) - 0.055;
+    t->invg[i] = (uint16_t)nearbyint(255.0 * v);
+  }
+  /* forward rows X, Y, Z; columns in BGR order (src[0] = B) */
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      t->cf[r * 3 + c] = (int32_t)nearbyint(4096.0 * kRgb2Xyz[r * 3 + (2 - c)] / kD65[r]);
+  /* inverse rows B, G, R; columns X, Y, Z */
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      t->ci[r * 3 + c] = (int32_t)nearbyint(4096.0 * kXyz2Rgb[(2 - r) * 3 + c] * kD65[c]);
+}
+
+static OracleLab g_olab;
+static int g_olab_ready = 0;
+static const OracleLab* olab(void) {
+  if (!g_olab_ready) {
+    oracle_lab_tables(&g_olab);
+    g_olab_ready = 1;
+  }
+  return &g_olab;
+}
+
+/* RGB2Lab_b: CV_DESCALE(x, n) = (x + 2^(n-1)) >> n (arithmetic shift). */
+static void bgr2lab_px(const OracleLab* t, int b, int g, int r, int* L, int* A, int* B) {
+  int B_ = t->gamma[b], G_ = t->gamma[g], R_ = t->gamma[r];
+  int X = (t->cf[0] * B_ + t->cf[1] * G_ + t->cf[2] * R_ + 2048) >> 12;
+  int Y = (t->cf[3] * B_ + t->cf[4] * G_ + t->cf[5] * R_ + 2048) >> 12;
+  int Z = (t->cf[6] * B_ + t->cf[7] * G_ + t->cf[8] * R_ + 2048) >> 12;
+  int fX = t->cbrt[X], fY = t->cbrt[Y], fZ = t->cbrt[Z];
+  *L = sat_u8((296 * fY - 1336934 + (1 << 14)) >> 15);
+  *A = sat_u8((500 * (fX - fY) + 128 * (1 << 15) + (1 << 14)) >> 15);
+  *B = sat_u8((200 * (fY - fZ) + 128 * (1 << 15) + (1 << 14)) >> 15);
+}
+
+static int ab_to_xz(int v) {
+  return v <= 3390 ? v * 108 / 841 - 16384 * 16 / 116 * 108 / 841 : v * v / 16384 * v / 16384;
+}
+
+/* Lab2RGBinteger::process, BGR output. */
+static void lab2bgr_px(const OracleLab* t, int L, int a, int b, int* ob, int* og, int* orr) {
+  int y = t->yf[2 * L], ify = t->yf[2 * L + 1];
+  int adiv = ((5 * a * 53687 + (1 << 7)) >> 13) - 128 * 16384 / 500;
+  int bdiv = ((b * 41943 + (1 << 4)) >> 9) - 128 * 16384 / 200 + 1;
+  int x = ab_to_xz(ify + adiv), z = ab_to_xz(ify - bdiv);
+  int o[3];
+  for (int r = 0; r < 3; ++r) {
+    int v = (t->ci[r * 3] * x + t->ci[r * 3 + 1] * y + t->ci[r * 3 + 2] * z + (1 << 13)) >> 14;
+    v = clampi(v, 0, 4095);
+    o[r] = t->invg[v];
+  }
+  *ob = o[0];
+  *og = o[1];
+  *orr = o[2];
+}
+
+void oracle_bgr2lab(const uint8_t* in, uint8_t* out, int n) {
+  const OracleLab* t = olab();
+  for (int i = 0; i < n; ++i) {
+    int L, A, B;
+    bgr2lab_px(t, in[3 * i], in[3 * i + 1], in[3 * i + 2], &L, &A, &B);
+    out[3 * i] = (uint8_t)L;
+    out[3 * i + 1] = (uint8_t)A;
+    out[3 * i + 2] = (uint8_t)B;
+  }
+}
+
+void oracle_lab2bgr(const uint8_t* in, uint8_t* out, int n) {
+  const OracleLab* t = olab();
+  for (int i = 0; i < n; ++i) {
+    int b, g, r;
+    lab2bgr_px(t, in[3 * i], in[3 * i + 1], in[3 * i + 2], &b, &g, &r);
+    out[3 * i] = (uint8_t)b;
+    out[3 * i + 1] = (uint8_t)g;
+    out[3 * i + 2] = (uint8_t)r;
+  }
+}
+
+/* CLAHEDehaze LAB path on one BGR frame (pitch = 3W). */
+void oracle_clahe_lab(const uint8_t* in, uint8_t* out, int H, int W, int tiles, double clip) {
+  size_t n = (size_t)H * W;
+  uint8_t* lab = (uint8_t*)malloc(n * 3);
+  uint8_t* l = (uint8_t*)malloc(n);
+  uint8_t* l2 = (uint8_t*)malloc(n);
+  oracle_bgr2lab(in, lab, (int)n);
+  for (size_t i = 0; i < n; ++i) l[i] = lab[3 * i];
+  oracle_clahe_u8c1(l, l2, H, W, tiles, clip);
+  for (size_t i = 0; i < n; ++i) lab[3 * i] = l2[i];
+  oracle_lab2bgr(lab, out, (int)n);
+  free(lab);
+  free(l);
+  free(l2);
+}

@@ -13,6 +13,9 @@
 //
 // HBM layout: frames are B x H x pitch bytes (interleaved BGR).  The LUT
 // workspace is B x tiles^2 x 256 u8 (16 KB per frame at 8x8).
+#include <cstring>
+#include <mutex>
+#include "lab.h"
 #include "lbgeo.h"
 
 namespace rv {
@@ -50,6 +53,17 @@ static ClaheGeo make_geo(int H, int W, int tiles, double clip) {
   return g;
 }
 
+// Lab tables (lab.h) in device memory, filled once on first LAB use.
+__device__ LabTables g_lab;
+
+enum ClaheSpace { kYCrCb = 0, kLab = 1 };
+
+template <int SPACE>
+__device__ __forceinline__ int clahe_luma(int b, int g, int r) {
+  if (SPACE == kLab) return lab_l(g_lab, b, g, r);
+  return bgr_to_y(b, g, r);
+}
+
 // ---------------------------------------------------------------------------
 // Kernel A: per (tile, frame) histogram of Y -> clip -> redistribute -> LUT.
 // One 256-thread workgroup per tile.  16 LDS histogram copies (wave x lane
@@ -57,6 +71,7 @@ static ClaheGeo make_geo(int H, int W, int tiles, double clip) {
 // Y values in a wave (flat sky / asphalt) spread over 4 addresses instead of
 // serialising on one, with no bank conflicts between the copies.
 // ---------------------------------------------------------------------------
+template <int SPACE>
 __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restrict__ in,
                                                         uint8_t* __restrict__ lut, int H, int W,
                                                         int pitch, ClaheGeo g) {
@@ -104,10 +119,10 @@ __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restric
         if (i0 + u * 256 >= total) break;
         const uint32_t w0 = w[u][0], w1 = w[u][1], w2 = w[u][2];
         // bytes little-endian: w0 = b0 g0 r0 b1 | w1 = g1 r1 b2 g2 | w2 = r2 b3 g3 r3
-        atomicAdd(&h[bgr_to_y(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255) * kCopies], 1);
-        atomicAdd(&h[bgr_to_y(w0 >> 24, w1 & 255, (w1 >> 8) & 255) * kCopies], 1);
-        atomicAdd(&h[bgr_to_y((w1 >> 16) & 255, w1 >> 24, w2 & 255) * kCopies], 1);
-        atomicAdd(&h[bgr_to_y((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24) * kCopies], 1);
+        atomicAdd(&h[clahe_luma<SPACE>(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255) * kCopies], 1);
+        atomicAdd(&h[clahe_luma<SPACE>(w0 >> 24, w1 & 255, (w1 >> 8) & 255) * kCopies], 1);
+        atomicAdd(&h[clahe_luma<SPACE>((w1 >> 16) & 255, w1 >> 24, w2 & 255) * kCopies], 1);
+        atomicAdd(&h[clahe_luma<SPACE>((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24) * kCopies], 1);
       }
     }
   } else {
@@ -120,7 +135,7 @@ __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restric
       int sx = x0 + c;
       if (sx >= W) sx = reflect101(sx, W);
       const uint8_t* p = frame + (size_t)sy * pitch + (size_t)sx * 3;
-      atomicAdd(&h[bgr_to_y(p[0], p[1], p[2]) * kCopies], 1);
+      atomicAdd(&h[clahe_luma<SPACE>(p[0], p[1], p[2]) * kCopies], 1);
     }
   }
   __syncthreads();
@@ -188,6 +203,7 @@ __device__ __forceinline__ int clahe_blend(int l11, int l12, int l21, int l22, c
 // ---------------------------------------------------------------------------
 constexpr int kApplyRows = 8;
 
+template <int SPACE>
 __global__ __launch_bounds__(256) void clahe_apply_kernel(const uint8_t* __restrict__ in,
                                                           uint8_t* __restrict__ out,
                                                           const uint8_t* __restrict__ lut, int H,
@@ -206,12 +222,18 @@ __global__ __launch_bounds__(256) void clahe_apply_kernel(const uint8_t* __restr
     uint8_t* dst = fout + (size_t)y * pitch;
     for (int x = threadIdx.x; x < W; x += 256) {
       const Interp ix = interp_axis(x, g.inv_tw, g.tiles);
-      int Y, Cr, Cb;
-      bgr_to_ycrcb(src[3 * x], src[3 * x + 1], src[3 * x + 2], Y, Cr, Cb);
+      int Y, Cr, Cb;  // (L, a, b) for SPACE == kLab
+      if (SPACE == kLab)
+        bgr_to_lab(g_lab, src[3 * x], src[3 * x + 1], src[3 * x + 2], Y, Cr, Cb);
+      else
+        bgr_to_ycrcb(src[3 * x], src[3 * x + 1], src[3 * x + 2], Y, Cr, Cb);
       const int y2 = clahe_blend(r1[ix.i1 * 256 + Y], r1[ix.i2 * 256 + Y], r2[ix.i1 * 256 + Y],
                                  r2[ix.i2 * 256 + Y], ix, iy);
       int bb, gg, rr;
-      ycrcb_to_bgr(y2, Cr, Cb, bb, gg, rr);
+      if (SPACE == kLab)
+        lab_to_bgr(g_lab, y2, Cr, Cb, bb, gg, rr);
+      else
+        ycrcb_to_bgr(y2, Cr, Cb, bb, gg, rr);
       dst[3 * x] = (uint8_t)bb;
       dst[3 * x + 1] = (uint8_t)gg;
       dst[3 * x + 2] = (uint8_t)rr;
@@ -827,8 +849,8 @@ extern "C" int rv_clahe_ycrcb_u8(const uint8_t* in, uint8_t* out, int B, int H, 
   ClaheGeo g = make_geo(H, W, tiles, clip);
   hipStream_t s = as_stream(stream);
   uint8_t* lut = (uint8_t*)ws;
-  clahe_lut_kernel<<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
-  clahe_apply_kernel<<<dim3(1, ceil_div(H, kApplyRows), B), 256, 0, s>>>(in, out, lut, H, W,
+  clahe_lut_kernel<kYCrCb><<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  clahe_apply_kernel<kYCrCb><<<dim3(1, ceil_div(H, kApplyRows), B), 256, 0, s>>>(in, out, lut, H, W,
                                                                           pitch, g);
   return launch_status("rv_clahe_ycrcb_u8");
 }
@@ -847,6 +869,51 @@ extern "C" int rv_median_u8c3(const uint8_t* in, uint8_t* out, int B, int H, int
   return launch_status("rv_median_u8c3");
 }
 
+static LabTables g_lab_host;
+static std::once_flag g_lab_once;
+static hipError_t g_lab_status = hipSuccess;
+
+static int ensure_lab_tables() {
+  std::call_once(g_lab_once, [] {
+    build_lab_tables(g_lab_host);
+    g_lab_status = hipMemcpyToSymbol(HIP_SYMBOL(g_lab), &g_lab_host, sizeof(LabTables));
+  });
+  if (g_lab_status != hipSuccess) {
+    set_error("Lab table upload: %s", hipGetErrorString(g_lab_status));
+    return -(int)g_lab_status;
+  }
+  return RV_OK;
+}
+
+extern "C" int rv_lab_init(void) { return ensure_lab_tables(); }
+
+extern "C" int rv_lab_tables_host(void* out, size_t bytes) {
+  RV_CHECK_ARG(out != nullptr && bytes == sizeof(LabTables), "need %zu bytes",
+               sizeof(LabTables));
+  LabTables t;
+  build_lab_tables(t);
+  memcpy(out, &t, sizeof(t));
+  return RV_OK;
+}
+
+extern "C" int rv_clahe_lab_u8(const uint8_t* in, uint8_t* out, int B, int H, int W, int pitch,
+                               int tiles, double clip, void* ws, size_t ws_bytes, void* stream) {
+  int st = check_frames(in, out, B, H, W, pitch);
+  if (st) return st;
+  RV_CHECK_ARG(tiles >= 1 && tiles <= 64, "tiles %d out of range", tiles);
+  RV_CHECK_ARG(ws != nullptr && ws_bytes >= rv_clahe_ws_bytes(B, tiles), "workspace too small");
+  st = ensure_lab_tables();
+  if (st) return st;
+  if (B == 0) return RV_OK;
+  ClaheGeo g = make_geo(H, W, tiles, clip);
+  hipStream_t s = as_stream(stream);
+  uint8_t* lut = (uint8_t*)ws;
+  clahe_lut_kernel<kLab><<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  clahe_apply_kernel<kLab><<<dim3(1, ceil_div(H, kApplyRows), B), 256, 0, s>>>(in, out, lut, H,
+                                                                              W, pitch, g);
+  return launch_status("rv_clahe_lab_u8");
+}
+
 extern "C" int rv_clahe_median_u8(const uint8_t* in, uint8_t* out, int B, int H, int W, int pitch,
                                   int tiles, double clip, int k, void* ws, size_t ws_bytes,
                                   void* stream) {
@@ -860,7 +927,7 @@ extern "C" int rv_clahe_median_u8(const uint8_t* in, uint8_t* out, int B, int H,
   hipStream_t s = as_stream(stream);
   uint8_t* lut = (uint8_t*)ws;
   if (k == 3 && med3_cells_fit(g, H, W)) {
-    clahe_lut_kernel<<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+    clahe_lut_kernel<kYCrCb><<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
     launch_med3<true, false>(in, out, lut, B, H, W, pitch, g, LbFuse{}, s);
     return launch_status("rv_clahe_median_u8");
   }
@@ -868,7 +935,7 @@ extern "C" int rv_clahe_median_u8(const uint8_t* in, uint8_t* out, int B, int H,
                "LUT window too large for the fused pass (tiles=%d, tile %dx%d); "
                "use rv_clahe_ycrcb_u8 + rv_median_u8c3",
                tiles, g.tw, g.th);
-  clahe_lut_kernel<<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  clahe_lut_kernel<kYCrCb><<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
   dispatch_median<true>(k, in, out, lut, B, H, W, pitch, g, s);
   return launch_status("rv_clahe_median_u8");
 }
@@ -908,7 +975,7 @@ extern "C" int rv_clahe_median_letterbox_u8(const uint8_t* in, uint8_t* out, int
   uint8_t* lut = (uint8_t*)ws;
   st = launch_letterbox_pad(lb_out, B, lb.g, s);
   if (st) return st;
-  clahe_lut_kernel<<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  clahe_lut_kernel<kYCrCb><<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
   launch_med3<true, true>(in, out, lut, B, H, W, pitch, g, lb, s);
   return launch_status("rv_clahe_median_letterbox_u8");
 }

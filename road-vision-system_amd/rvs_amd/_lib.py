@@ -34,6 +34,10 @@ _SIGS = {
     "rv_clahe_ws_bytes": (c_size_t, [c_int, c_int]),
     "rv_clahe_ycrcb_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                   c_double, c_void_p, c_size_t, c_void_p]),
+    "rv_clahe_lab_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                c_double, c_void_p, c_size_t, c_void_p]),
+    "rv_lab_init": (c_int, []),
+    "rv_lab_tables_host": (c_int, [c_void_p, c_size_t]),
     "rv_median_u8c3": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "rv_clahe_median_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                    c_double, c_int, c_void_p, c_size_t, c_void_p]),

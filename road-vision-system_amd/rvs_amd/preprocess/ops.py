@@ -46,15 +46,12 @@ def _back(t, was_numpy):
 
 
 class CLAHEDehaze(PreprocessOp):
-    """CLAHE on the luma channel (YCrCb path), HIP kernels."""
+    """CLAHE on the luma channel, HIP kernels: YCrCb (default) or LAB
+    (clahe_dehaze.py:21-30; any space other than "LAB" takes YCrCb)."""
 
     def __init__(self, **params):
         super().__init__(**params)
         self.space, self.clip_limit, self.grid = clahe_params(self.params)
-        if self.space == "LAB":
-            # LAB is the off-by-default branch (clahe_dehaze.py:21-25); its
-            # OpenCV 8U Lab tables are not restated yet (SURVEY 8(f) item 1).
-            raise NotImplementedError("CLAHEDehaze space='LAB' is not implemented on HIP yet")
         self._ws = None
 
     def __call__(self, image):
@@ -63,7 +60,8 @@ class CLAHEDehaze(PreprocessOp):
         need = kernels.clahe_ws_bytes(B, self.grid)
         if self._ws is None or self._ws.numel() < need or self._ws.device != x.device:
             self._ws = torch.empty(need, dtype=torch.uint8, device=x.device)
-        out = kernels.clahe_ycrcb(x, self.grid, self.clip_limit, ws=self._ws)
+        fn = kernels.clahe_lab if self.space == "LAB" else kernels.clahe_ycrcb
+        out = fn(x, self.grid, self.clip_limit, ws=self._ws)
         return _back(out, was_np)
 
 

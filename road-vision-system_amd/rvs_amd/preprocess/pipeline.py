@@ -29,8 +29,9 @@ class PreprocessPipeline:
             params = node.get("params", {})
             cls = get_op_class(name)
             self.ops.append(cls(**params))
+        # the fused CLAHE+median passes are YCrCb-only; a LAB chain runs op by op
         self._fused = (len(self.ops) == 2 and isinstance(self.ops[0], CLAHEDehaze)
-                       and isinstance(self.ops[1], MedianDerain))
+                       and self.ops[0].space != "LAB" and isinstance(self.ops[1], MedianDerain))
         self._ws = None
 
     def _gate_enabled(self) -> bool:

@@ -140,3 +140,74 @@ def test_letterbox_identity_at_640():
     img = road_frame(640, 640, seed=4)
     geo = cpu.letterbox_geometry(640, 640)
     np.testing.assert_array_equal(cpu.letterbox(img, geo), img)
+
+
+# --- LAB path (clahe_dehaze.py:21-25) ------------------------------------
+def _cie_lab8(bgr):
+    """Float CIE L*a*b* (sRGB, D65) scaled to OpenCV's 8U ranges."""
+    c = bgr[..., ::-1].astype(np.float64) / 255.0
+    lin = np.where(c <= 0.04045, c / 12.92, ((c + 0.055) / 1.055) ** 2.4)
+    m = np.array([[0.412453, 0.357580, 0.180423], [0.212671, 0.715160, 0.072169],
+                  [0.019334, 0.119193, 0.950227]])
+    xyz = lin @ m.T / np.array([0.950456, 1.0, 1.088754])
+    f = np.where(xyz > 216 / 24389, np.cbrt(xyz), xyz * 841 / 108 + 16 / 116)
+    L = 116 * f[..., 1] - 16
+    a = 500 * (f[..., 0] - f[..., 1])
+    b = 200 * (f[..., 1] - f[..., 2])
+    return np.stack([L * 255 / 100, a + 128, b + 128], -1)
+
+
+def test_lab_known_answers():
+    px = np.array([[[255, 255, 255], [0, 0, 0], [128, 128, 128], [0, 0, 255], [0, 255, 0],
+                    [255, 0, 0]]], np.uint8)
+    lab = cpu.bgr2lab(px)
+    assert lab[0, 0].tolist() == [255, 128, 128] and lab[0, 1].tolist() == [0, 128, 128]
+    # CIE values: red (53.24, 80.09, 67.20), green (87.73, -86.18, 83.18),
+    # blue (32.30, 79.19, -107.86), gray 128 (53.59, 0, 0)
+    assert lab[0, 2].tolist() == [137, 128, 128]
+    assert lab[0, 3].tolist() == [136, 208, 195]
+    assert lab[0, 4].tolist() == [224, 42, 211]
+    assert lab[0, 5].tolist() == [82, 207, 20]
+    back = cpu.lab2bgr(lab)
+    assert back[0, 0].tolist() == [255, 255, 255] and back[0, 1].tolist() == [0, 0, 0]
+    assert back[0, 2].tolist() == [128, 128, 128]
+
+
+def test_lab_matches_cie_float():
+    rng = np.random.default_rng(0)
+    x = rng.integers(0, 256, (1, 50000, 3), dtype=np.uint8)
+    d = np.abs(cpu.bgr2lab(x).astype(np.float64) - _cie_lab8(x))
+    # the 11-bit linear-light table quantises dark colours: measured max 2.1
+    # LSB (a channel), > 1 LSB for 0.3 % of values
+    assert d.max() <= 2.5 and (d > 1.0).mean() < 0.01, d.max()
+    # the inverse recovers grays within 1 LSB (L has 256 levels over 0..100)
+    # and colours within the 8U Lab quantisation (measured max 22 on
+    # saturated colours, mean < 1)
+    g = np.repeat(np.arange(256, dtype=np.uint8)[None, :, None], 3, 2)
+    rg = cpu.lab2bgr(cpu.bgr2lab(g)).astype(int)
+    assert np.abs(rg - g).max() <= 1
+    rt = np.abs(cpu.lab2bgr(cpu.bgr2lab(x)).astype(int) - x)
+    assert rt.mean() < 1.0 and rt.max() <= 24
+
+
+def test_lab_tables_in_library_match_oracle():
+    import ctypes
+    from rvs_amd import _lib
+    buf = ctypes.create_string_buffer(cpu.LAB_TABLE_BYTES)
+    assert _lib.load().rv_lab_tables_host(buf, cpu.LAB_TABLE_BYTES) == 0
+    assert buf.raw == cpu.lab_tables()
+    assert _lib.load().rv_lab_tables_host(buf, 100) == -1000
+
+
+def test_clahe_lab_oracle_structure():
+    img = road_frame(120, 160, seed=4)
+    out = cpu.clahe_lab(img, 8, 2.0)
+    lab_in, lab_out = cpu.bgr2lab(img), cpu.bgr2lab(out)
+    # CLAHE equalises L: the L spread grows on a low-contrast road frame
+    spread = lambda p: np.percentile(p, 95) - np.percentile(p, 5)  # noqa: E731
+    assert spread(lab_out[..., 0]) > spread(lab_in[..., 0])
+    # the L plane CLAHE'd by the oracle is exactly what the chain applies
+    l2 = cpu.clahe_u8c1(np.ascontiguousarray(lab_in[..., 0]), 8, 2.0)
+    merged = lab_in.copy()
+    merged[..., 0] = l2
+    np.testing.assert_array_equal(out, cpu.lab2bgr(merged))

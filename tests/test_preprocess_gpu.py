@@ -145,3 +145,31 @@ def test_fused_letterbox_equals_chain(cuda, H, W):
     np.testing.assert_array_equal(lb.cpu().numpy(), kernels.letterbox(chain, geo).cpu().numpy())
     ref = cpu.letterbox(cpu.median(cpu.clahe_ycrcb(img, 8, 2.0), 3), geo)
     np.testing.assert_array_equal(lb[0].cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("H,W,tiles,clip", [(1080, 1920, 8, 2.0), (640, 640, 8, 2.0),
+                                            (37, 91, 3, 2.0), (480, 640, 8, 0.0),
+                                            (721, 1283, 5, 4.0)])
+def test_clahe_lab_bit_exact(cuda, H, W, tiles, clip):
+    """CLAHEDehaze space='LAB' (rv_clahe_lab_u8) vs the C oracle, bit-exact."""
+    from rvs_amd import kernels
+    B = 2
+    frames = np.stack([road_frame(H, W, seed=60 + b) for b in range(B)])
+    frames[1, : H // 3] = (frames[1, : H // 3].astype(int) * [1, 1, 2] // [1, 1, 1]
+                           ).clip(0, 255).astype(np.uint8)  # saturated reds
+    got = kernels.clahe_lab(_dev(frames, cuda), tiles, clip).cpu().numpy()
+    for b in range(B):
+        np.testing.assert_array_equal(got[b], cpu.clahe_lab(frames[b], tiles, clip))
+
+
+def test_lab_chain_through_pipeline(cuda):
+    from rvs_amd.preprocess import PreprocessPipeline
+    cfg = {"enabled": True,
+           "chain": [{"name": "CLAHEDehaze", "params": {"space": "lab", "clip_limit": 2.0,
+                                                         "tile_grid": 8}},
+                     {"name": "MedianDerain", "params": {"ksize": 3}}]}
+    p = PreprocessPipeline(cfg)
+    assert not p._fused  # the fused passes are YCrCb-only
+    img = road_frame(360, 640, seed=12)
+    out = p(img)
+    np.testing.assert_array_equal(out, cpu.median(cpu.clahe_lab(img, 8, 2.0), 3))
