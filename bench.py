@@ -106,12 +106,14 @@ def main():
 
     from rvs_amd import _lib
     from rvs_amd.engine import OverlappedSteps, RoadVisionEngine
+    from rvs_amd.shard import job_throughput, max_over_ranks, rank_streams
     from rvs_amd.synth import road_frames
 
     cfg = bench_config()
     S, K, Wm = args.streams, args.steps, args.warmup
     eng = RoadVisionEngine(cfg, S, (H, W), device=dev)
-    frames = road_frames(S, Wm + K, H, W, device=dev, stream_offset=rank * S)
+    frames = road_frames(S, Wm + K, H, W, device=dev,
+                         stream_offset=rank_streams(S, rank).start)
     ts_all = torch.tensor([[f / 30.0] * S for f in range(Wm + K)], dtype=torch.float64,
                           device=dev)
     torch.cuda.synchronize()
@@ -151,9 +153,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         torch.distributed.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dev)
 
     # live conv timing (HIP events on the launch stream): a separate eager
     # pass over the same K steps (event records cannot live inside graphs)
@@ -188,8 +188,7 @@ def main():
     tp = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
     if os.path.exists(tp):
         traffic = json.load(open(tp)).get("conv_bytes_per_step")
-    total_frames = world * S * K
-    value = total_frames / elapsed
+    value = job_throughput(S * K, world, elapsed)
     res = {
         "metric": "end-to-end frames/sec @1080p (preproc+YOLOv8n+SORT), 1/2/4/8 MI355X",
         "value": round(value, 2),
