@@ -255,9 +255,12 @@ int rv_sort_export(const void* state, int S, int tmax, double* x_out, int* meta,
 #define RV_FOG_NPARAM 16
 /* consts (host, RV_FOG_NCONST f32): {vx, vy, dv_max, d_min, d_range, 0,
  *   rain_p, rain_len, n_oct, [gh, gw, amp, 0] x 4 octaves, norm}.
- * scene (device f32, 4*H + W): per-row 0.7*dp/dp_max, depth factor
- *   (sky boost x road damp), global-veil weight, airlight vertical gradient;
- *   then the per-column airlight horizontal gradient.
+ * scene (device f32, 4*H + W + 3*n_oct*(H + W)): per-row 0.7*dp/dp_max,
+ *   depth factor (sky boost x road damp), global-veil weight, airlight
+ *   vertical gradient; the per-column airlight horizontal gradient; then per
+ *   octave the noise sample taps: rows {y0[H], y1[H], wy[H]}, columns
+ *   {x0[W], x1[W], wx[W]} (ys = (y*gh)/H in f32, y0 = floor, y1 = min(y0+1,
+ *   gh), wy = ys - y0; the same along x).
  * frame_params (device, B x RV_FOG_NPARAM f32): {beta, A_b, A_g, A_r,
  *   A_scale, tint_b, tint_g, tint_r, gamma, rain_seed (< 2^24), 0...}.
  * grids (device, B x grid_stride f32): per frame, the octaves' value-noise

@@ -48,18 +48,22 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
 
 // Raw (un-normalised) fBM value noise at pixel (y, x): rand_perlin
 // (fog.py:8-41) with ys = (y*gh)/h in f32, bilinear on the per-frame grid.
+// The per-axis sample taps (y0, y1, wy) / (x0, x1, wx) of every octave are
+// resolution-only, so the host computes them once (same f32 values) and the
+// kernel reads them from the scene buffer: no divides or floors per pixel.
 __device__ __forceinline__ float noise_at(const FogConsts& c, const float* __restrict__ g,
-                                          int y, int x, int H, int W) {
+                                          const float* __restrict__ taps, int y, int x, int H,
+                                          int W) {
   float base = 0.f;
   for (int j = 0; j < c.n_oct; ++j) {
-    const int gh = c.gh[j], gw = c.gw[j];
-    const float ys = (float)(y * gh) / (float)H;
-    const float xs = (float)(x * gw) / (float)W;
-    const int y0 = (int)floorf(ys), x0 = (int)floorf(xs);
-    const int y1 = min(y0 + 1, gh), x1 = min(x0 + 1, gw);
-    const float wy = ys - (float)y0, wx = xs - (float)x0;
+    const float* ty = taps + (size_t)j * 3 * (H + W);
+    const float* tx = ty + 3 * H;
+    const int y0 = (int)ty[y], y1 = (int)ty[H + y];
+    const float wy = ty[2 * H + y];
+    const int x0 = (int)tx[x], x1 = (int)tx[W + x];
+    const float wx = tx[2 * W + x];
     const float* gj = g + c.goff[j];
-    const int rw = gw + 1;
+    const int rw = c.gw[j] + 1;
     const float g00 = gj[y0 * rw + x0], g01 = gj[y0 * rw + x1];
     const float g10 = gj[y1 * rw + x0], g11 = gj[y1 * rw + x1];
     const float top = g00 * (1.f - wx) + g01 * wx;
@@ -78,6 +82,7 @@ __device__ __forceinline__ float noise_at(const FogConsts& c, const float* __res
 constexpr int kRangeBlocks = 256;
 
 __global__ __launch_bounds__(256) void fog_range_kernel(const float* __restrict__ grids,
+                                                        const float* __restrict__ taps,
                                                         FogConsts c, int H, int W,
                                                         float* __restrict__ part) {
   const int b = blockIdx.y;
@@ -85,7 +90,7 @@ __global__ __launch_bounds__(256) void fog_range_kernel(const float* __restrict_
   float mn = INFINITY, mx = -INFINITY;
   const int n = H * W;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const float v = noise_at(c, g, i / W, i % W, H, W);
+    const float v = noise_at(c, g, taps, i / W, i % W, H, W);
     mn = fminf(mn, v);
     mx = fmaxf(mx, v);
   }
@@ -141,9 +146,8 @@ __global__ __launch_bounds__(256) void fog_range_finish(const float* __restrict_
 }
 
 // One output channel value, fog.py:271-296 (f32, contract off).
-__device__ __forceinline__ int fog_channel(int u, float t, float A, float gv, float tint,
+__device__ __forceinline__ int fog_channel(float v, float t, float A, float gv, float tint,
                                            float gamma, bool rain) {
-  const float v = (float)u / 255.f;
   float h = v * t + A * (1.f - t);
   h = fminf(fmaxf(h * (1.f - gv) + A * gv, 0.f), 1.f);
   h = fminf(fmaxf(h * tint, 0.f), 1.f);
@@ -157,6 +161,9 @@ __global__ __launch_bounds__(256) void fog_apply_kernel(
     const uint8_t* __restrict__ in, uint8_t* __restrict__ out, int H, int W, int pitch,
     const float* __restrict__ scene, const float* __restrict__ fparams,
     const float* __restrict__ grids, FogConsts c, const float* __restrict__ range) {
+  __shared__ float inv255[256];  // u / 255.f, exactly as the scalar divide
+  inv255[threadIdx.x] = (float)threadIdx.x / 255.f;
+  __syncthreads();
   const int b = blockIdx.y;
   const float* fp = fparams + (size_t)b * RV_FOG_NPARAM;
   const float beta0 = fp[0], Ab = fp[1], Ag = fp[2], Ar = fp[3], Asc = fp[4];
@@ -169,6 +176,7 @@ __global__ __launch_bounds__(256) void fog_apply_kernel(
   const float* row_gv = scene + 2 * H;
   const float* row_vg = scene + 3 * H;
   const float* col_xg = scene + 4 * H;
+  const float* taps = scene + 4 * H + W;
   const int gpr = W / V;  // pixel groups per row
   const size_t fofs = (size_t)b * H * pitch;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < H * gpr;
@@ -194,7 +202,7 @@ __global__ __launch_bounds__(256) void fog_apply_kernel(
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const int x = x0 + k;
-      const float n = noise_at(c, g, y, x, H, W);
+      const float n = noise_at(c, g, taps, y, x, H, W);
       const float nn = (n - mn) / fmaxf(1e-6f, mx - mn);
       const float beta = beta0 * (0.85f + 0.35f * nn);
       const float dx = (float)x - c.vx;
@@ -214,9 +222,9 @@ __global__ __launch_bounds__(256) void fog_apply_kernel(
             lowbias32(rseed ^ lowbias32(col * 0x9E3779B1u + lowbias32((uint32_t)seg)));
         rain = hsh < c.rain_thresh;
       }
-      px[3 * k + 0] = (uint8_t)fog_channel(px[3 * k + 0], t, Ab_, gv, tb, gamma, rain);
-      px[3 * k + 1] = (uint8_t)fog_channel(px[3 * k + 1], t, Ag_, gv, tg, gamma, rain);
-      px[3 * k + 2] = (uint8_t)fog_channel(px[3 * k + 2], t, Ar_, gv, tr, gamma, rain);
+      px[3 * k + 0] = (uint8_t)fog_channel(inv255[px[3 * k + 0]], t, Ab_, gv, tb, gamma, rain);
+      px[3 * k + 1] = (uint8_t)fog_channel(inv255[px[3 * k + 1]], t, Ag_, gv, tg, gamma, rain);
+      px[3 * k + 2] = (uint8_t)fog_channel(inv255[px[3 * k + 2]], t, Ar_, gv, tr, gamma, rain);
     }
     if (V == 4) {
       uint32_t* d32 = (uint32_t*)dst;
@@ -285,7 +293,8 @@ extern "C" int rv_fog_rain_u8(const uint8_t* in, uint8_t* out, int B, int H, int
   float* range = (float*)ws;
   float* part = range + 2 * (size_t)B;
   const int rblocks = min(kRangeBlocks, ceil_div(H * W, 256));
-  fog_range_kernel<<<dim3(rblocks, B), 256, 0, s>>>(grids, c, H, W, part);
+  fog_range_kernel<<<dim3(rblocks, B), 256, 0, s>>>(grids, scene + 4 * H + W, c, H, W,
+                                                      part);
   fog_range_finish<<<B, 256, 0, s>>>(part, rblocks, range);
   const bool vec = (W % 4 == 0) && (pitch % 4 == 0) && (((uintptr_t)in | (uintptr_t)out) % 4 == 0);
   if (vec) {

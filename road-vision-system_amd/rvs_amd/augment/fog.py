@@ -125,7 +125,14 @@ class FogSynthesizer:
                 consts[9 + 4 * j:12 + 4 * j] = [gh, gw, amp]
             consts[25] = norm
             stride = sum((gh + 1) * (gw + 1) for gh, gw, _ in octs)
-            scene = torch.from_numpy(np.concatenate([rows.ravel(), cols])).to(self.device)
+            taps = []
+            for gh, gw, _ in octs:  # noise sample taps (rand_perlin, fog.py:24-31)
+                for n, gn in ((h, gh), (w, gw)):
+                    s = (np.arange(n) * gn).astype(_F) / _F(n)
+                    i0 = np.floor(s)
+                    taps += [i0, np.minimum(i0 + 1, gn).astype(_F), (s - i0).astype(_F)]
+            scene = torch.from_numpy(np.concatenate([rows.ravel(), cols] + taps)
+                                     .astype(_F)).to(self.device)
             self._scenes[key] = (consts, scene, octs, stride)
         return self._scenes[key]
 
