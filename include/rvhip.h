@@ -243,6 +243,34 @@ int rv_sort_update(void* state_in, void* state_out, int S, int tmax, const float
 int rv_sort_export(const void* state, int S, int tmax, double* x_out, int* meta, int* T_out,
                    void* stream);
 
+/* --- Standalone pieces of SortTracker.update / GroundProjector, batched over
+ * S streams (csrc/track_ops.hip; rv_sort_update fuses the same math). */
+/* _iou_matrix (sort_tracker.py:74-80, _iou :55-71) in f32 scalar order.
+ * trk: S x Tmax x 4, det: S x Dmax x 4 (x1,y1,x2,y2) f32; T[S], D[S] valid
+ * counts (device).  out: S x Tmax x Dmax, zero outside T[s] x D[s]. */
+int rv_iou_matrix_batched(const float* trk, const int* T, const float* det, const int* D,
+                          float* out, int S, int Tmax, int Dmax, void* stream);
+/* _associate's greedy loop (sort_tracker.py:196-208): argmax (first max in
+ * row-major order), stop below thr (f64 compare), accept if row and column
+ * are free, mask both with -1.  M (S x Tmax x Dmax, e.g. from
+ * rv_iou_matrix_batched) is modified in place like the reference's matrix.
+ * Outputs (device): match_t / match_d (S x min(Tmax, Dmax)) in acceptance
+ * order, n_match[S], trk_match (S x Tmax: det index or -1), det_match
+ * (S x Dmax: track index or -1); the reference's unmatched lists are the
+ * -1 entries in ascending order.  thr <= -1 (an endless loop in the
+ * reference) stops once every row is masked. */
+int rv_greedy_assign_batched(float* M, const int* T, const int* D, int S, int Tmax, int Dmax,
+                             double thr, int* match_t, int* match_d, int* n_match,
+                             int* trk_match, int* det_match, void* stream);
+/* GroundProjector.project_bbox + distance (projector.py:30-47, 74-84): foot
+ * point (0.5*(x1+x2), y2) through the f64 homography H9 (device, row-major);
+ * out_xy (n x 2 f64, NaN = None); out_dist (nullable, n f64, NaN = None):
+ * f32 norm to origin2 (device, nullable = no distance), capped at
+ * max_distance when >= 0. */
+int rv_homography_project_f64(const double* H9, const float* boxes, int n,
+                              const float* origin2, double max_distance,
+                              double* out_xy, double* out_dist, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* Augment: fog + rain synthetic inputs (EnhancedFogSynthesizer.synthesize,  */
 /* src/augment/fog.py:239-299; tools/fog_batch.py:7-34 drives it offline).   */

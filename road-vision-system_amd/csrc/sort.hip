@@ -23,6 +23,7 @@
 #include <string.h>
 #include <vector>
 #include "common.h"
+#include "track_math.h"
 
 namespace rv {
 
@@ -77,19 +78,6 @@ __device__ __forceinline__ float4 x_to_bbox(const double* x) {
   const double h = s / fmax(1e-6, w);
   return make_float4((float)(cx - 0.5 * w), (float)(cy - 0.5 * h), (float)(cx + 0.5 * w),
                      (float)(cy + 0.5 * h));
-}
-
-// _iou in numpy float32 scalar arithmetic
-__device__ __forceinline__ float iou_f32(float4 a, float4 b) {
-  const float ix1 = fmaxf(a.x, b.x), iy1 = fmaxf(a.y, b.y);
-  const float ix2 = fminf(a.z, b.z), iy2 = fminf(a.w, b.w);
-  const float iw = fmaxf(0.0f, ix2 - ix1), ih = fmaxf(0.0f, iy2 - iy1);
-  const float inter = iw * ih;
-  const float area_a = fmaxf(0.0f, a.z - a.x) * fmaxf(0.0f, a.w - a.y);
-  const float area_b = fmaxf(0.0f, b.z - b.x) * fmaxf(0.0f, b.w - b.y);
-  const float denom = area_a + area_b - inter;
-  if (denom <= 0.0f) return 0.0f;
-  return inter / denom;
 }
 
 // _update_motion_matrix(dt) + kf.predict()
@@ -200,24 +188,13 @@ __device__ void kf_update(Track& t, const double z[4]) {
     }
 }
 
-// HomographyProjector.project_point / GroundProjector.distance
+// HomographyProjector.project_point / GroundProjector.distance (track_math.h)
 __device__ __forceinline__ bool project(const SortParams& p, double x, double y, double& X,
                                         double& Y) {
-  const double mx = p.H[0] * x + p.H[1] * y + p.H[2];
-  const double my = p.H[3] * x + p.H[4] * y + p.H[5];
-  const double w = p.H[6] * x + p.H[7] * y + p.H[8];
-  if (fabs(w) < 1e-6) return false;
-  X = mx / w;
-  Y = my / w;
-  return isfinite(X) && isfinite(Y);
+  return project_h(p.H, x, y, X, Y);
 }
 __device__ __forceinline__ double distance(const SortParams& p, double X, double Y) {
-  const float vx = (float)X - p.origin[0], vy = (float)Y - p.origin[1];
-  const float d = sqrtf(vx * vx + vy * vy);
-  if (!isfinite(d)) return NAN;
-  double dd = (double)d;
-  if (p.max_distance >= 0.0) dd = fmin(dd, p.max_distance);
-  return dd;
+  return distance_o(p.origin, p.max_distance, X, Y);
 }
 
 // _Track.update_metrics

@@ -48,6 +48,14 @@ _SIGS = {
     "rv_clahe_median_letterbox_fits": (c_int, [c_int, c_int, c_int, c_int, POINTER(c_int)]),
     "rv_gray_span_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                 c_void_p]),
+    # standalone tracker / geometry pieces
+    "rv_iou_matrix_batched": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                      c_int, c_int, c_void_p]),
+    "rv_greedy_assign_batched": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                         c_double, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p]),
+    "rv_homography_project_f64": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_double,
+                                          c_void_p, c_void_p, c_void_p]),
     # augment
     "rv_fog_ws_bytes": (c_size_t, [c_int]),
     "rv_fog_rain_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,

@@ -74,6 +74,10 @@ class MultiStreamSort:
         self.cur = 1 - self.cur
         return self.out_id, self.out_dist, self.out_speed
 
+    def update_many(self, streams, timestamps) -> List[List[Detection]]:
+        """Tracker.update over all S streams at once (module update_many)."""
+        return update_many(self, streams, timestamps)
+
     def export(self):
         """Host copy of every stream's tracks: (T[S], x[S,tmax,7], meta[S,tmax,4])."""
         x = torch.empty((self.S, self.tmax, 7), dtype=torch.float64, device=self.device)
@@ -82,6 +86,79 @@ class MultiStreamSort:
         call("rv_sort_export", ptr(self.state[self.cur]), self.S, self.tmax, ptr(x), ptr(meta),
              ptr(T), stream_ptr())
         return T.cpu().numpy(), x.cpu().numpy(), meta.cpu().numpy()
+
+
+def update_many(core: "MultiStreamSort", streams, timestamps) -> List[List[Detection]]:
+    """Tracker.update for S camera streams in one launch: `streams` is a list
+    of S detection lists (one frame per stream), `timestamps` S seconds.
+    Mutates and returns the Detection objects like SortTracker.update."""
+    lists = [list(x) for x in streams]
+    S = core.S
+    if len(lists) != S or len(timestamps) != S:
+        raise ValueError(f"expected {S} streams and timestamps")
+    rows = np.zeros((S, core.dmax, 6), np.float32)
+    cnt = np.zeros(S, np.int32)
+    for s, lst in enumerate(lists):
+        if len(lst) > core.dmax:
+            raise ValueError(f"{len(lst)} detections exceed dmax={core.dmax}")
+        cnt[s] = len(lst)
+        for i, d in enumerate(lst):
+            rows[s, i] = (d.x1, d.y1, d.x2, d.y2, d.conf, d.cls_id)
+    dev = core.device
+    tid, dist, spd = core.update(torch.from_numpy(rows).to(dev), torch.from_numpy(cnt).to(dev),
+                                 torch.tensor([float(t) for t in timestamps], dtype=torch.float64,
+                                              device=dev))
+    tid, dist, spd = tid.cpu().numpy(), dist.cpu().numpy(), spd.cpu().numpy()
+    for s, lst in enumerate(lists):
+        for i, d in enumerate(lst):
+            d.track_id = None if tid[s, i] < 0 else int(tid[s, i])
+            d.distance_m = None if np.isnan(dist[s, i]) else float(dist[s, i])
+            d.speed_kmh = None if np.isnan(spd[s, i]) else float(spd[s, i])
+    return lists
+
+
+def iou_matrix_batched(trk: torch.Tensor, T: torch.Tensor, det: torch.Tensor,
+                       D: torch.Tensor) -> torch.Tensor:
+    """_iou_matrix (sort_tracker.py:74-80) for S streams: trk (S,Tmax,4),
+    det (S,Dmax,4) f32 device, T/D (S,) int32 counts -> (S,Tmax,Dmax)."""
+    S, Tmax, _ = trk.shape
+    Dmax = det.shape[1]
+    out = torch.empty((S, Tmax, Dmax), dtype=torch.float32, device=trk.device)
+    call("rv_iou_matrix_batched", ptr(trk.contiguous()), ptr(T), ptr(det.contiguous()), ptr(D),
+         ptr(out), S, Tmax, Dmax, stream_ptr())
+    return out
+
+
+def associate_batched(M: torch.Tensor, T: torch.Tensor, D: torch.Tensor, thr: float):
+    """_associate's greedy loop (sort_tracker.py:196-208) on (S,Tmax,Dmax)
+    IoU matrices (modified in place).  Returns (match_t, match_d, n_match,
+    trk_match, det_match) device tensors."""
+    S, Tmax, Dmax = M.shape
+    mc = min(Tmax, Dmax)
+    dev = M.device
+    mt = torch.empty((S, mc), dtype=torch.int32, device=dev)
+    md = torch.empty((S, mc), dtype=torch.int32, device=dev)
+    n = torch.empty(S, dtype=torch.int32, device=dev)
+    tm = torch.empty((S, Tmax), dtype=torch.int32, device=dev)
+    dm = torch.empty((S, Dmax), dtype=torch.int32, device=dev)
+    call("rv_greedy_assign_batched", ptr(M), ptr(T), ptr(D), S, Tmax, Dmax, float(thr), ptr(mt),
+         ptr(md), ptr(n), ptr(tm), ptr(dm), stream_ptr())
+    return mt, md, n, tm, dm
+
+
+def project_boxes(H: torch.Tensor, boxes: torch.Tensor, origin: Optional[torch.Tensor] = None,
+                  max_distance: Optional[float] = None):
+    """GroundProjector.project_bbox + distance (projector.py:30-47) for n
+    boxes: H (3,3) f64, boxes (n,4) f32, origin (2,) f32 -> (xy (n,2) f64,
+    dist (n,) f64); NaN = None."""
+    n = boxes.shape[0]
+    dev = boxes.device
+    xy = torch.empty((n, 2), dtype=torch.float64, device=dev)
+    dist = torch.empty(n, dtype=torch.float64, device=dev)
+    call("rv_homography_project_f64", ptr(H.contiguous()), ptr(boxes.contiguous()), n,
+         ptr(origin) if origin is not None else None,
+         -1.0 if max_distance is None else float(max_distance), ptr(xy), ptr(dist), stream_ptr())
+    return xy, dist
 
 
 class SortTracker(Tracker):
@@ -130,3 +207,4 @@ class SortTracker(Tracker):
 
     def close(self) -> None:
         self.core.reset()
+
