@@ -21,6 +21,14 @@ inline int launch_status(const char* what) {
   return RV_OK;
 }
 
+// A HIP runtime call's status as an ABI code (RV_OK or -(hipError_t)), with
+// the call named in rv_last_error() when it failed.
+inline int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return RV_OK;
+  set_error("%s: %s", what, hipGetErrorString(e));
+  return -(int)e;
+}
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }

@@ -1419,7 +1419,8 @@ int launch_stem(const uint8_t* img, int B, int H, int W, const float* w0, const 
   const size_t smem = (size_t)kStXB + kStLB;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)stem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    // best effort: a failure surfaces as the launch error reported below
+    (void)hipFuncSetAttribute((const void*)stem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024);
     (void)hipGetLastError();
     attr = true;
@@ -1534,7 +1535,8 @@ int launch_sppf_pool(bf16_t* buf, int B, int H, int W, int c, hipStream_t s) {
   }
   static bool attr = false;
   if (!attr && smem > 64 * 1024) {  // only raise the cap when a map needs it
-    hipFuncSetAttribute((const void*)sppf_pool_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    // best effort: a failure surfaces as the launch error reported below
+    (void)hipFuncSetAttribute((const void*)sppf_pool_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                         kSppfLds);
     (void)hipGetLastError();
     attr = true;
@@ -1823,7 +1825,8 @@ int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_ma
   const bool fused = lv[0].feat != nullptr;
   static bool attr[2] = {false, false};
   if (!attr[fused] && smem > 64 * 1024) {  // only raise the cap when the head needs it
-    hipFuncSetAttribute(fused ? (const void*)detect_decode_kernel<16, true>
+    // best effort: a failure surfaces as the launch error reported below
+    (void)hipFuncSetAttribute(fused ? (const void*)detect_decode_kernel<16, true>
                               : (const void*)detect_decode_kernel<16, false>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();

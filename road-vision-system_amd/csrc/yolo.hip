@@ -207,9 +207,10 @@ struct Model {
   hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
   ~Model() {
     for (int i = 0; i < 2; ++i) {
-      if (side[i]) hipStreamDestroy(side[i]);
-      if (ev_fork[i]) hipEventDestroy(ev_fork[i]);
-      if (ev_join[i]) hipEventDestroy(ev_join[i]);
+      // teardown: a failure here leaves nothing to report or undo
+      if (side[i]) (void)hipStreamDestroy(side[i]);
+      if (ev_fork[i]) (void)hipEventDestroy(ev_fork[i]);
+      if (ev_join[i]) (void)hipEventDestroy(ev_join[i]);
     }
   }
   int max_B = 0, H = 0, W = 0;
@@ -405,12 +406,18 @@ struct Exec {
     M->launches.push_back(a);
     Profile& P = M->prof;
     const bool rec = P.on && P.n_fwd < P.cap_fwd && li_ < P.per_fwd;
-    if (rec) hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + li_) * 2], s);
+    const int ev0 =
+        rec ? hip_check(hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + li_) * 2], s),
+                        "profile hipEventRecord")
+            : RV_OK;
     if (li_ < (int)M->tuned.size() && M->tuned[li_].mr > 0 && conv_cfg_ok(a, M->tuned[li_]))
       status = launch_conv_cfg(a, M->tuned[li_], s);
     else
       status = launch_conv(a, s);
-    if (rec) hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + li_) * 2 + 1], s);
+    if (!status) status = ev0;
+    if (rec && !status)
+      status = hip_check(hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + li_) * 2 + 1], s),
+                         "profile hipEventRecord");
     if (P.on && P.n_fwd == 0 && li_ < P.per_fwd) {
       P.flops[li_] = flops;
       P.bytes[li_] = launch_bytes(a);
@@ -714,13 +721,15 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   };
   auto forked_head = [&](int i) {  // level i's head on side stream i (joined before decode)
     if (!fork) return head_level(i);
-    hipEventRecord(M->ev_fork[i], main_s);
-    hipStreamWaitEvent(M->side[i], M->ev_fork[i], 0);
+    int e = hip_check(hipEventRecord(M->ev_fork[i], main_s), "head fork hipEventRecord");
+    if (!e) e = hip_check(hipStreamWaitEvent(M->side[i], M->ev_fork[i], 0), "head fork wait");
+    if (e) return E.status = e;
     E.s = M->side[i];
     const int r = head_level(i);
-    hipEventRecord(M->ev_join[i], M->side[i]);
+    e = hip_check(hipEventRecord(M->ev_join[i], M->side[i]), "head join hipEventRecord");
     E.s = main_s;
-    return r;
+    if (!r && e) E.status = e;
+    return r ? r : e;
   };
   E.c2f("model.15", View{M->CAT14, cat14, 0}, 3, M->C15, v.h15, v.nb, false,
         View{M->X15, v.h15, 0});
@@ -734,7 +743,8 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
         View{M->X21, v.h21, 0});
   if (E.status || head_level(2)) return E.status;
   if (fork)
-    for (int i = 0; i < 2; ++i) hipStreamWaitEvent(main_s, M->ev_join[i], 0);
+    for (int i = 0; i < 2 && !E.status; ++i)
+      E.status = hip_check(hipStreamWaitEvent(main_s, M->ev_join[i], 0), "head join wait");
   if (E.status) return E.status;
   if (M->prof.on && M->prof.n_fwd < M->prof.cap_fwd) M->prof.n_fwd++;
   HeadLevel hl[3];
@@ -796,7 +806,7 @@ extern "C" int rv_yolo_profile(void* h, int max_forwards) {
   RV_CHECK_ARG(h && max_forwards >= 0, "bad args");
   Model* M = (Model*)h;
   Profile& P = M->prof;
-  for (hipEvent_t e : P.ev) hipEventDestroy(e);
+  for (hipEvent_t e : P.ev) (void)hipEventDestroy(e);  // teardown
   P.ev.clear();
   P.on = max_forwards > 0;
   P.n_fwd = 0;
@@ -904,19 +914,21 @@ extern "C" int rv_yolo_autotune(void* h, const uint8_t* lb, int B, void* ws, siz
     if (verify)
       for (int d = 0; d < 2; ++d)
         if (out_bytes(a, d))
-          hipMemcpyAsync(ref + d * maxb, d == 0 ? a.out0 : a.out1, out_bytes(a, d),
-                         hipMemcpyDeviceToDevice, s);
+          if (!st)
+            st = hip_check(hipMemcpyAsync(ref + d * maxb, d == 0 ? a.out0 : a.out1,
+                                          out_bytes(a, d), hipMemcpyDeviceToDevice, s),
+                           "autotune reference copy");
     auto time_cfg = [&](const ConvCfg* c) -> float {
       int r = c ? launch_conv_cfg(a, *c, s) : launch_conv(a, s);  // warm-up launch
-      hipEventRecord(e0, s);
+      if (!r) r = hip_check(hipEventRecord(e0, s), "autotune hipEventRecord");
       for (int k = 0; k < reps && !r; ++k) r = c ? launch_conv_cfg(a, *c, s) : launch_conv(a, s);
-      hipEventRecord(e1, s);
+      if (!r) r = hip_check(hipEventRecord(e1, s), "autotune hipEventRecord");
       if (r || hipEventSynchronize(e1) != hipSuccess) {
         if (!st) st = r ? r : RV_EINVAL;
         return 1e30f;
       }
       float ms = 0.f;
-      hipEventElapsedTime(&ms, e0, e1);
+      if (hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return 1e30f;  // never chosen
       return ms / reps;
     };
     const float t0 = time_cfg(nullptr);
@@ -929,13 +941,16 @@ extern "C" int rv_yolo_autotune(void* h, const uint8_t* lb, int B, void* ws, siz
         for (int d = 0; d < 2; ++d) {
           const size_t nb = out_bytes(a, d);
           if (!nb) continue;
-          hipMemsetAsync(cnt, 0, sizeof(unsigned), s);
+          int vs = hip_check(hipMemsetAsync(cnt, 0, sizeof(unsigned), s), "autotune verify");
           count_diff_kernel<<<1024, 256, 0, s>>>((const uint32_t*)(ref + d * maxb),
                                                  (const uint32_t*)(d == 0 ? a.out0 : a.out1),
                                                  nb / 4, cnt);
           unsigned h_cnt = 0;
-          hipMemcpyAsync(&h_cnt, cnt, sizeof(unsigned), hipMemcpyDeviceToHost, s);
-          hipStreamSynchronize(s);
+          if (!vs)
+            vs = hip_check(hipMemcpyAsync(&h_cnt, cnt, sizeof(unsigned), hipMemcpyDeviceToHost, s),
+                           "autotune verify");
+          if (!vs) vs = hip_check(hipStreamSynchronize(s), "autotune verify");
+          if (vs && !st) st = vs;
           diff += h_cnt;
         }
         if (diff) ++bad;
@@ -951,10 +966,11 @@ extern "C" int rv_yolo_autotune(void* h, const uint8_t* lb, int B, void* ws, siz
               i, a.Ho, a.Wo, a.k, a.stride, a.Cin, a.Cout, t0 * 1e3, tbest * 1e3, best[i].mr,
               best[i].nr, best[i].G, best[i].resw, best[i].persist, best[i].kind, n);
   }
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  if (ref) hipFree(ref);
-  if (cnt) hipFree(cnt);
+  // teardown of the autotuner's private buffers: nothing to report
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (ref) (void)hipFree(ref);
+  if (cnt) (void)hipFree(cnt);
   if (n_bad) *n_bad = bad;
   if (!st) M->tuned = best;
   return st;
