@@ -272,6 +272,18 @@ int rv_homography_project_f64(const double* H9, const float* boxes, int n,
                               double* out_xy, double* out_dist, void* stream);
 
 /* ------------------------------------------------------------------------ */
+/* Ingest: NV12 -> BGR (cv2.COLOR_YUV2BGR_NV12, 8U, BT.601 video range,      */
+/* 20-bit fixed point).  The device half of a decode front end for           */
+/* src/io_video/capture.py:10-24: host-fed NV12 is 1.5 B/pixel over PCIe     */
+/* instead of 3.  y: B frames of H x W (y_pitch, y_frame_stride bytes apart); */
+/* uv: interleaved U,V, H/2 x W (uv_pitch, uv_frame_stride); H, W even.      */
+/* A packed NV12 batch is y = base, uv = base + H*W, both strides H*W*3/2.   */
+/* ------------------------------------------------------------------------ */
+int rv_nv12_to_bgr_u8(const uint8_t* y, const uint8_t* uv, int y_pitch, int uv_pitch,
+                      size_t y_frame_stride, size_t uv_frame_stride, uint8_t* out,
+                      int B, int H, int W, int pitch, void* stream);
+
+/* ------------------------------------------------------------------------ */
 /* Augment: fog + rain synthetic inputs (EnhancedFogSynthesizer.synthesize,  */
 /* src/augment/fog.py:239-299; tools/fog_batch.py:7-34 drives it offline).   */
 /* Restated subset: depth proxy, value-noise beta map, transmission, airlight */

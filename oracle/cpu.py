@@ -38,6 +38,7 @@ def lib():
         L.oracle_bgr2lab.argtypes = [c_void_p, c_void_p, c_int]
         L.oracle_lab2bgr.argtypes = [c_void_p, c_void_p, c_int]
         L.oracle_lab_tables.argtypes = [c_void_p]
+        L.oracle_nv12_to_bgr.argtypes = [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int]
         L.oracle_ycrcb2bgr.argtypes = [c_void_p, c_void_p, c_int]
         L.oracle_median_u8c3.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int]
         L.oracle_letterbox_geometry.argtypes = [c_int, c_int, c_int, c_int, POINTER(c_int)]
@@ -85,6 +86,17 @@ def lab2bgr(img):
     img = np.ascontiguousarray(img, dtype=np.uint8)
     out = np.empty_like(img)
     lib().oracle_lab2bgr(_p(img), _p(out), img.size // 3)
+    return out
+
+
+def nv12_to_bgr(y: np.ndarray, uv: np.ndarray) -> np.ndarray:
+    """cv2.COLOR_YUV2BGR_NV12 (BT.601 video range, 20-bit fixed point):
+    y (H, W) u8, uv (H/2, W) u8 interleaved U,V -> (H, W, 3) BGR."""
+    y = np.ascontiguousarray(y, dtype=np.uint8)
+    uv = np.ascontiguousarray(uv, dtype=np.uint8)
+    H, W = y.shape
+    out = np.empty((H, W, 3), np.uint8)
+    lib().oracle_nv12_to_bgr(_p(y), _p(uv), W, W, _p(out), H, W)
     return out
 
 

@@ -543,3 +543,31 @@ void oracle_clahe_lab(const uint8_t* in, uint8_t* out, int H, int W, int tiles, 
   free(l);
   free(l2);
 }
+
+/* ------------------------------------------------------------------------
+ * cv2.cvtColor(COLOR_YUV2BGR_NV12), 8U (OpenCV color_yuv: YUV420sp2RGB8,
+ * ITU-R BT.601 video range, 20-bit fixed point).  The device half of a
+ * decode front end (src/io_video/capture.py:10-24 hands BGR frames to the
+ * pipeline; a hardware decoder hands NV12).  Y plane H x W (y_pitch), then
+ * the interleaved U,V plane H/2 x W (uv_pitch); H and W even.
+ * ---------------------------------------------------------------------- */
+void oracle_nv12_to_bgr(const uint8_t* y, const uint8_t* uv, int y_pitch, int uv_pitch,
+                        uint8_t* out, int H, int W) {
+  const int CY = 1220542, CUB = 2116026, CUG = -409993, CVG = -852492, CVR = 1673527;
+  const int SH = 20;
+  for (int r = 0; r < H; ++r)
+    for (int c = 0; c < W; ++c) {
+      const int u = uv[(r / 2) * uv_pitch + (c & ~1)] - 128;
+      const int v = uv[(r / 2) * uv_pitch + (c & ~1) + 1] - 128;
+      const int ruv = (1 << (SH - 1)) + CVR * v;
+      const int guv = (1 << (SH - 1)) + CVG * v + CUG * u;
+      const int buv = (1 << (SH - 1)) + CUB * u;
+      int yy = y[r * y_pitch + c] - 16;
+      if (yy < 0) yy = 0;
+      yy *= CY;
+      uint8_t* o = out + ((size_t)r * W + c) * 3;
+      o[0] = (uint8_t)sat_u8((yy + buv) >> SH);
+      o[1] = (uint8_t)sat_u8((yy + guv) >> SH);
+      o[2] = (uint8_t)sat_u8((yy + ruv) >> SH);
+    }
+}

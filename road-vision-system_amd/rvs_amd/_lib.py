@@ -56,6 +56,9 @@ _SIGS = {
                                          c_void_p, c_void_p]),
     "rv_homography_project_f64": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_double,
                                           c_void_p, c_void_p, c_void_p]),
+    # ingest
+    "rv_nv12_to_bgr_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_size_t, c_size_t, c_void_p,
+                                  c_int, c_int, c_int, c_int, c_void_p]),
     # augment
     "rv_fog_ws_bytes": (c_size_t, [c_int]),
     "rv_fog_rain_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,

@@ -77,6 +77,28 @@ def clahe_lab(frames: torch.Tensor, tiles: int = 8, clip: float = 2.0,
     return out if frames.dim() == 4 else out[0]
 
 
+def nv12_to_bgr(nv12: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Packed NV12 frames (B, 3H/2, W) u8 on device (Y rows, then interleaved
+    U,V rows) -> (B, H, W, 3) BGR, cv2.COLOR_YUV2BGR_NV12 bit for bit."""
+    if nv12.dim() == 2:
+        return nv12_to_bgr(nv12.unsqueeze(0), None if out is None else out.unsqueeze(0))[0]
+    if nv12.dim() != 3 or nv12.dtype != torch.uint8 or not nv12.is_cuda:
+        raise ValueError("expected packed NV12 uint8 (B, 3H/2, W) on the GPU")
+    nv12 = nv12.contiguous()
+    B, R, W = nv12.shape
+    if R % 3 or (2 * R // 3) % 2 or W % 2:
+        raise ValueError(f"NV12 rows {R} / width {W}: need 3H/2 rows with H, W even")
+    H = 2 * R // 3
+    if out is None:
+        out = torch.empty((B, H, W, 3), dtype=torch.uint8, device=nv12.device)
+    elif out.shape != (B, H, W, 3) or not out.is_contiguous():
+        raise ValueError("out must be a contiguous (B, H, W, 3) uint8 tensor")
+    fs = R * W
+    call("rv_nv12_to_bgr_u8", ptr(nv12), nv12.data_ptr() + H * W, W, W, fs, fs, ptr(out), B, H, W,
+         3 * W, stream_ptr())
+    return out
+
+
 def median(frames: torch.Tensor, k: int = 3, out: Optional[torch.Tensor] = None):
     x, B, H, W, pitch = _frames(frames)
     out = _like(x, out)

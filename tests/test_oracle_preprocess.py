@@ -211,3 +211,39 @@ def test_clahe_lab_oracle_structure():
     merged = lab_in.copy()
     merged[..., 0] = l2
     np.testing.assert_array_equal(out, cpu.lab2bgr(merged))
+
+
+# --- NV12 ingest (cv2.COLOR_YUV2BGR_NV12) ----------------------------------
+def test_nv12_known_answers():
+    uv = np.array([[128, 128]], np.uint8)
+    assert cpu.nv12_to_bgr(np.full((2, 2), 16, np.uint8), uv)[0, 0].tolist() == [0, 0, 0]
+    assert cpu.nv12_to_bgr(np.full((2, 2), 235, np.uint8), uv)[0, 0].tolist() == [255, 255, 255]
+    # BT.601 video-range primaries (Y, U, V) -> BGR
+    red = cpu.nv12_to_bgr(np.full((2, 2), 81, np.uint8), np.array([[90, 240]], np.uint8))
+    blue = cpu.nv12_to_bgr(np.full((2, 2), 41, np.uint8), np.array([[240, 110]], np.uint8))
+    assert red[0, 0].tolist() == [0, 0, 254] and blue[0, 0].tolist() == [255, 0, 0]
+
+
+def test_nv12_matches_bt601_float():
+    rng = np.random.default_rng(5)
+    H, W = 64, 96
+    y = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    uv = rng.integers(0, 256, (H // 2, W), dtype=np.uint8)
+    got = cpu.nv12_to_bgr(y, uv).astype(np.float64)
+    u = np.repeat(np.repeat(uv[:, 0::2].astype(np.float64) - 128, 2, 0), 2, 1)
+    v = np.repeat(np.repeat(uv[:, 1::2].astype(np.float64) - 128, 2, 0), 2, 1)
+    yy = 1.164 * np.maximum(y.astype(np.float64) - 16, 0)
+    ref = np.stack([yy + 2.018 * u, yy - 0.391 * u - 0.813 * v, yy + 1.596 * v], -1)
+    d = np.abs(got - np.clip(ref, 0, 255))
+    assert d.max() <= 1.5  # fixed-point truncation vs the rounded float matrix
+
+
+def test_nv12_abi_argument_errors():
+    import ctypes
+    from rvs_amd import _lib
+    lib = _lib.load()
+    p = ctypes.c_void_p(64)
+    assert lib.rv_nv12_to_bgr_u8(None, p, 4, 4, 24, 8, p, 1, 4, 4, 12, None) == -1000
+    assert lib.rv_nv12_to_bgr_u8(p, p, 4, 4, 24, 8, p, 1, 3, 4, 12, None) == -1000  # odd H
+    assert lib.rv_nv12_to_bgr_u8(p, p, 4, 4, 8, 8, p, 1, 4, 4, 12, None) == -1000  # stride
+    assert lib.rv_nv12_to_bgr_u8(p, p, 4, 4, 24, 8, p, 0, 4, 4, 12, None) == 0  # B = 0

@@ -173,3 +173,18 @@ def test_lab_chain_through_pipeline(cuda):
     img = road_frame(360, 640, seed=12)
     out = p(img)
     np.testing.assert_array_equal(out, cpu.median(cpu.clahe_lab(img, 8, 2.0), 3))
+
+
+@pytest.mark.parametrize("H,W,B", [(1080, 1920, 3), (2, 2, 1), (6, 10, 2), (480, 642, 2)])
+def test_nv12_to_bgr_bit_exact(cuda, H, W, B):
+    """rv_nv12_to_bgr_u8 vs the C oracle (cv2.COLOR_YUV2BGR_NV12), bit-exact;
+    W % 4 != 0 takes the scalar path."""
+    import torch
+    from rvs_amd import kernels
+    rng = np.random.default_rng(H + W)
+    nv = rng.integers(0, 256, (B, H * 3 // 2, W), dtype=np.uint8)
+    got = kernels.nv12_to_bgr(torch.from_numpy(nv).to(cuda)).cpu().numpy()
+    for b in range(B):
+        np.testing.assert_array_equal(got[b], cpu.nv12_to_bgr(nv[b, :H], nv[b, H:]))
+    one = kernels.nv12_to_bgr(torch.from_numpy(nv[0]).to(cuda)).cpu().numpy()
+    np.testing.assert_array_equal(one, got[0])
