@@ -80,7 +80,7 @@ def cpu_baseline(frames_host: np.ndarray, ts: np.ndarray, cfg: dict, threads: in
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=60)  # pipeline fill/drain < 1 %
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--streams", type=int, default=32, help="camera streams per GPU")
     ap.add_argument("--cpu-frames", type=int, default=int(os.environ.get("RV_CPU_FRAMES", 6)))
