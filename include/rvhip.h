@@ -61,8 +61,9 @@ int rv_clahe_ycrcb_u8(const uint8_t* in, uint8_t* out, int B, int H, int W,
 /* CLAHEDehaze space="LAB" (clahe_dehaze.py:21-25): cv2.COLOR_BGR2LAB, CLAHE
  * on L, cv2.COLOR_LAB2BGR, 8U sRGB / D65 integer paths (OpenCV color_lab.cpp
  * RGB2Lab_b / Lab2RGBinteger, restated; csrc/lab.h).  Same arguments and
- * workspace as rv_clahe_ycrcb_u8.  The first LAB call uploads the Lab tables
- * synchronously; call rv_lab_init() once before capturing it in a graph. */
+ * workspace as rv_clahe_ycrcb_u8.  The first LAB call on a device uploads
+ * the Lab tables to it synchronously; call rv_lab_init() (current device)
+ * once before capturing the op in a graph. */
 int rv_clahe_lab_u8(const uint8_t* in, uint8_t* out, int B, int H, int W,
                     int pitch, int tiles, double clip, void* ws,
                     size_t ws_bytes, void* stream);

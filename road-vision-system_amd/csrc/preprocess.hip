@@ -870,19 +870,24 @@ extern "C" int rv_median_u8c3(const uint8_t* in, uint8_t* out, int B, int H, int
 }
 
 static LabTables g_lab_host;
-static std::once_flag g_lab_once;
-static hipError_t g_lab_status = hipSuccess;
+static std::once_flag g_lab_built;
+static std::mutex g_lab_mu;
+static uint64_t g_lab_devices = 0;  // bit d: tables uploaded to device d
 
+// Upload the Lab tables to the current device once (per device: a process
+// may drive several GPUs).  Synchronous; call rv_lab_init() before capture.
 static int ensure_lab_tables() {
-  std::call_once(g_lab_once, [] {
-    build_lab_tables(g_lab_host);
-    g_lab_status = hipMemcpyToSymbol(HIP_SYMBOL(g_lab), &g_lab_host, sizeof(LabTables));
-  });
-  if (g_lab_status != hipSuccess) {
-    set_error("Lab table upload: %s", hipGetErrorString(g_lab_status));
-    return -(int)g_lab_status;
-  }
-  return RV_OK;
+  std::call_once(g_lab_built, [] { build_lab_tables(g_lab_host); });
+  int dev = 0;
+  int st = hip_check(hipGetDevice(&dev), "hipGetDevice");
+  if (st) return st;
+  RV_CHECK_ARG(dev >= 0 && dev < 64, "device %d out of range", dev);
+  std::lock_guard<std::mutex> lock(g_lab_mu);
+  if (g_lab_devices >> dev & 1) return RV_OK;
+  st = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_lab), &g_lab_host, sizeof(LabTables)),
+                 "Lab table upload");
+  if (!st) g_lab_devices |= 1ull << dev;
+  return st;
 }
 
 extern "C" int rv_lab_init(void) { return ensure_lab_tables(); }

@@ -59,19 +59,19 @@ def clahe_ycrcb(frames: torch.Tensor, tiles: int = 8, clip: float = 2.0,
     return out if frames.dim() == 4 else out[0]
 
 
-_lab_ready = False
+_lab_ready = set()  # devices whose Lab tables are uploaded
 
 
 def clahe_lab(frames: torch.Tensor, tiles: int = 8, clip: float = 2.0,
               out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None):
     """CLAHEDehaze space='LAB' (clahe_dehaze.py:21-25) on device frames."""
-    global _lab_ready
     x, B, H, W, pitch = _frames(frames)
     out = _like(x, out)
     ws, need = _ws(B, tiles, ws, x.device)
-    if not _lab_ready:  # one synchronous table upload, before any graph capture
-        call("rv_lab_init")
-        _lab_ready = True
+    if x.device not in _lab_ready:  # one synchronous upload per device, before capture
+        with torch.cuda.device(x.device):
+            call("rv_lab_init")
+        _lab_ready.add(x.device)
     call("rv_clahe_lab_u8", ptr(x), ptr(out), B, H, W, pitch, int(tiles), float(clip),
          ptr(ws), ws.numel(), stream_ptr())
     return out if frames.dim() == 4 else out[0]
