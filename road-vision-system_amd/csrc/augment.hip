@@ -17,7 +17,11 @@
 // allows it.  The value noise needs a per-frame min/max before it can be
 // normalised (fog.py:43), so a first pass reduces it (ALU only, no frame
 // bytes read, partials per workgroup, no atomics) and the second pass does
-// the per-pixel work.
+// the per-pixel work.  The per-pixel pass is VALU-bound, so its exp, pow and
+// divides use the hardware instructions (v_exp_f32 / v_log_f32 / v_rcp_f32,
+// about 1 ulp) instead of the IEEE library sequences; the oracle's bar (u8
+// |d| <= 1, >= 99 % exact) covers that.  The noise range pass keeps exact
+// divides.
 #include "common.h"
 
 namespace rv {
@@ -25,6 +29,7 @@ namespace rv {
 namespace {
 
 constexpr int kFogMaxOct = 4;
+constexpr int kGridLds = 2048;  // noise grid floats staged in LDS (8 KB)
 
 struct FogConsts {
   float vx, vy, dv_max, d_min, d_range, veil_unused, rain_p, rain_len;
@@ -85,15 +90,21 @@ __global__ __launch_bounds__(256) void fog_range_kernel(const float* __restrict_
                                                         const float* __restrict__ taps,
                                                         FogConsts c, int H, int W,
                                                         float* __restrict__ part) {
+  __shared__ float sgrid[kGridLds];  // this frame's value-noise grids
   const int b = blockIdx.y;
-  const float* g = grids + (size_t)b * c.grid_stride;
+  const bool grid_lds = c.grid_stride <= kGridLds;
+  if (grid_lds)
+    for (int i = threadIdx.x; i < c.grid_stride; i += blockDim.x)
+      sgrid[i] = grids[(size_t)b * c.grid_stride + i];
+  __syncthreads();
+  const float* g = grid_lds ? sgrid : grids + (size_t)b * c.grid_stride;
   float mn = INFINITY, mx = -INFINITY;
-  const int n = H * W;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const float v = noise_at(c, g, taps, i / W, i % W, H, W);
-    mn = fminf(mn, v);
-    mx = fmaxf(mx, v);
-  }
+  for (int y = blockIdx.x; y < H; y += gridDim.x)  // whole rows: no index divides
+    for (int x = threadIdx.x; x < W; x += blockDim.x) {
+      const float v = noise_at(c, g, taps, y, x, H, W);
+      mn = fminf(mn, v);
+      mx = fmaxf(mx, v);
+    }
   for (int o = 32; o > 0; o >>= 1) {
     mn = fminf(mn, __shfl_xor(mn, o));
     mx = fmaxf(mx, __shfl_xor(mx, o));
@@ -145,13 +156,24 @@ __global__ __launch_bounds__(256) void fog_range_finish(const float* __restrict_
   }
 }
 
+// Hardware transcendentals (about 1 ulp): 2^x, log2 x, 1/x.
+__device__ __forceinline__ float hw_exp(float x) {
+  return __builtin_amdgcn_exp2f(x * 1.44269504088896341f);
+}
+__device__ __forceinline__ float hw_pow01(float h, float g) {  // h in [0, 1]
+  return __builtin_amdgcn_exp2f(g * __builtin_amdgcn_logf(h));
+}
+__device__ __forceinline__ float hw_div(float a, float b) {
+  return a * __builtin_amdgcn_rcpf(b);
+}
+
 // One output channel value, fog.py:271-296 (f32, contract off).
 __device__ __forceinline__ int fog_channel(float v, float t, float A, float gv, float tint,
                                            float gamma, bool rain) {
   float h = v * t + A * (1.f - t);
   h = fminf(fmaxf(h * (1.f - gv) + A * gv, 0.f), 1.f);
   h = fminf(fmaxf(h * tint, 0.f), 1.f);
-  if (gamma != 1.f) h = fminf(fmaxf(powf(h, gamma), 0.f), 1.f);
+  if (gamma != 1.f) h = fminf(fmaxf(hw_pow01(h, gamma), 0.f), 1.f);
   if (rain) h = h + (1.f - h) * 0.45f;
   return (int)(h * 255.f + 0.5f);
 }
@@ -162,15 +184,20 @@ __global__ __launch_bounds__(256) void fog_apply_kernel(
     const float* __restrict__ scene, const float* __restrict__ fparams,
     const float* __restrict__ grids, FogConsts c, const float* __restrict__ range) {
   __shared__ float inv255[256];  // u / 255.f, exactly as the scalar divide
-  inv255[threadIdx.x] = (float)threadIdx.x / 255.f;
-  __syncthreads();
+  __shared__ float sgrid[kGridLds];  // this frame's value-noise grids
   const int b = blockIdx.y;
+  inv255[threadIdx.x] = (float)threadIdx.x / 255.f;
+  const bool grid_lds = c.grid_stride <= kGridLds;
+  if (grid_lds)
+    for (int i = threadIdx.x; i < c.grid_stride; i += blockDim.x)
+      sgrid[i] = grids[(size_t)b * c.grid_stride + i];
+  __syncthreads();
   const float* fp = fparams + (size_t)b * RV_FOG_NPARAM;
   const float beta0 = fp[0], Ab = fp[1], Ag = fp[2], Ar = fp[3], Asc = fp[4];
   const float tb = fp[5], tg = fp[6], tr = fp[7], gamma = fp[8];
   const uint32_t rseed = (uint32_t)fp[9];
   const float mn = range[2 * b], mx = range[2 * b + 1];
-  const float* g = grids + (size_t)b * c.grid_stride;
+  const float* g = grid_lds ? sgrid : grids + (size_t)b * c.grid_stride;
   const float* row_dp = scene;
   const float* row_fac = scene + H;
   const float* row_gv = scene + 2 * H;
@@ -203,14 +230,14 @@ __global__ __launch_bounds__(256) void fog_apply_kernel(
     for (int k = 0; k < V; ++k) {
       const int x = x0 + k;
       const float n = noise_at(c, g, taps, y, x, H, W);
-      const float nn = (n - mn) / fmaxf(1e-6f, mx - mn);
+      const float nn = hw_div(n - mn, fmaxf(1e-6f, mx - mn));
       const float beta = beta0 * (0.85f + 0.35f * nn);
       const float dx = (float)x - c.vx;
-      const float dv = 1.f / (sqrtf(dx * dx + dy * dy) + 1.f);
-      float d = dp + 0.3f * (dv / c.dv_max);
-      d = (d - c.d_min) / c.d_range;
+      const float dv = __builtin_amdgcn_rcpf(sqrtf(dx * dx + dy * dy) + 1.f);
+      float d = dp + 0.3f * hw_div(dv, c.dv_max);
+      d = hw_div(d - c.d_min, c.d_range);
       d = fminf(fmaxf(d * fac, 0.f), 1.f);
-      const float t = fminf(fmaxf(expf(-beta * d), 0.05f), 1.f);
+      const float t = fminf(fmaxf(hw_exp(-beta * d), 0.05f), 1.f);
       const float xg = col_xg[x];
       const float Ab_ = fminf(fmaxf(fminf(fmaxf(Ab * vg * xg, 0.7f), 1.f) * Asc, 0.75f), 1.f);
       const float Ag_ = fminf(fmaxf(fminf(fmaxf(Ag * vg * xg, 0.7f), 1.f) * Asc, 0.75f), 1.f);
