@@ -90,6 +90,8 @@ def main():
                     help="skip the per-layer conv kernel autotuning before the timed region")
     ap.add_argument("--depth", type=int, default=int(os.environ.get("RV_PIPE_DEPTH", 3)),
                     help="pipelined steps: 3 = Y(k) || P(k+1) || T(k-1), 2 = [T(k-1) || P(k)] -> Y(k)")
+    ap.add_argument("--graph-chunk", type=int, default=None,
+                    help="pipeline steps per captured graph (default 8, RV_GRAPH_CHUNK; 0 = all)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one graph per step; no overlap of step k's NMS+SORT with step k+1")
     args = ap.parse_args()
@@ -129,7 +131,8 @@ def main():
         # the track stage of step k (NMS + SORT, latency-bound) overlaps the
         # preprocess of step k+1 inside one graph (engine.OverlappedSteps)
         runner = OverlappedSteps(eng, [frames[Wm + k] for k in range(K)],
-                                 [ts_all[Wm + k] for k in range(K)], depth=args.depth)
+                                 [ts_all[Wm + k] for k in range(K)], depth=args.depth,
+                                 chunk=args.graph_chunk)
         torch.cuda.synchronize()
     elif not args.eager:
         # one HIP graph per timed step (its own frame batch); replayed in order
@@ -189,6 +192,9 @@ def main():
     if os.path.exists(tp):
         traffic = json.load(open(tp)).get("conv_bytes_per_step")
     value = job_throughput(S * K, world, elapsed)
+    chunk_desc = (args.graph_chunk if args.graph_chunk is not None
+                  else int(os.environ.get("RV_GRAPH_CHUNK", "8")))
+    chunk_desc = "all" if chunk_desc <= 0 else str(chunk_desc)
     res = {
         "metric": "end-to-end frames/sec @1080p (preproc+YOLOv8n+SORT), 1/2/4/8 MI355X",
         "value": round(value, 2),
@@ -212,7 +218,8 @@ def main():
                    "execution": "eager" if args.eager else
                                 ("graph per step" if args.no_pipeline else
                                  f"graphs, {args.depth}-stage software pipeline over steps "
-                                 "(preprocess / YOLO / NMS+SORT of consecutive steps overlap)")},
+                                 "(preprocess / YOLO / NMS+SORT of consecutive steps overlap), "
+                                 f"{chunk_desc} steps per graph")},
         "roofline": {
             "kernel": "conv family: conv_patch_kernel + conv1x1_direct_kernel (all YOLOv8n conv "
                       "launches of a step, HIP events on the launch stream)",

@@ -11,6 +11,7 @@ step.  ``results()`` converts one step's device outputs into the reference's
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -152,7 +153,8 @@ class OverlappedSteps:
     epilogue graph fills and drains the pipeline.  Replayed in order, the K
     steps give the same results as K step() calls (tests/test_engine_gpu.py)."""
 
-    def __init__(self, eng: "RoadVisionEngine", frames, ts, depth: int = 2):
+    def __init__(self, eng: "RoadVisionEngine", frames, ts, depth: int = 2,
+                 chunk: Optional[int] = None):
         self.eng = eng
         K = len(frames)
         dev = eng.device
@@ -180,25 +182,35 @@ class OverlappedSteps:
                 self.graphs.append(g)
             return
         lbs = {}
-        for j in range(-1, K + 1):
+        # steps per captured graph (`chunk`, RV_GRAPH_CHUNK): consecutive
+        # pipeline stages j are captured into one graph, so the device never
+        # idles between graph replays inside a chunk; 0 = all K+2 stages in
+        # one graph.  A serving loop replays one chunk per `chunk` steps.
+        if chunk is None:
+            chunk = int(os.environ.get("RV_GRAPH_CHUNK", "8"))
+        js = list(range(-1, K + 1))
+        size = len(js) if chunk <= 0 else chunk
+        for c0 in range(0, len(js), size):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                cur = torch.cuda.current_stream()
-                side_t.wait_stream(cur)
-                side_p.wait_stream(cur)
-                if j + 1 < K:  # P(j+1) into letterbox slot (j+1) % 2
-                    with torch.cuda.stream(side_p):
-                        procs[j + 1], lbs[j + 1] = eng.preprocess_stage(frames[j + 1], (j + 1) % 2)
-                if j >= 1:  # T(j-1) from candidate slot (j-1) % 2
-                    with torch.cuda.stream(side_t):
-                        out = eng.track_stage(ts[j - 1], (j - 1) % 2)
-                if 0 <= j < K:  # Y(j)
-                    eng.yolo_stage(lbs.pop(j), j % 2)
-                cur.wait_stream(side_p)
-                cur.wait_stream(side_t)
-                if j >= 1:
-                    out["proc"] = procs.pop(j - 1)
-                    self.outs.append(out)
+                for j in js[c0:c0 + size]:
+                    cur = torch.cuda.current_stream()
+                    side_t.wait_stream(cur)
+                    side_p.wait_stream(cur)
+                    if j + 1 < K:  # P(j+1) into letterbox slot (j+1) % 2
+                        with torch.cuda.stream(side_p):
+                            procs[j + 1], lbs[j + 1] = eng.preprocess_stage(frames[j + 1],
+                                                                            (j + 1) % 2)
+                    if j >= 1:  # T(j-1) from candidate slot (j-1) % 2
+                        with torch.cuda.stream(side_t):
+                            out = eng.track_stage(ts[j - 1], (j - 1) % 2)
+                    if 0 <= j < K:  # Y(j)
+                        eng.yolo_stage(lbs.pop(j), j % 2)
+                    cur.wait_stream(side_p)
+                    cur.wait_stream(side_t)
+                    if j >= 1:
+                        out["proc"] = procs.pop(j - 1)
+                        self.outs.append(out)
             self.graphs.append(g)
 
     def run(self):

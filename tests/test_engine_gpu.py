@@ -51,12 +51,13 @@ def test_engine_steps_match_oracle(cuda):
     eng.close()
 
 
-@pytest.mark.parametrize("depth", [2, 3])
-def test_overlapped_steps_match_sequential_steps(cuda, depth):
+@pytest.mark.parametrize("depth,chunk", [(2, None), (3, 1), (3, 3), (3, None), (3, 0)])
+def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk):
     """bench.py's timed mode (engine.OverlappedSteps): the track stage of step
-    k runs on a side stream beside the preprocess of step k+1.  The final
-    detections, track ids, proc frames and the whole SORT state must equal
-    those of plain sequential step() calls."""
+    k runs on a side stream beside the preprocess of step k+1, with `chunk`
+    pipeline stages per captured graph (None = the default 8, 0 = one graph).
+    The final detections, track ids, proc frames and the whole SORT state must
+    equal those of plain sequential step() calls."""
     from rvs_amd.config import load_config
     from rvs_amd.engine import OverlappedSteps, RoadVisionEngine
     from rvs_amd.synth import road_frames
@@ -73,7 +74,7 @@ def test_overlapped_steps_match_sequential_steps(cuda, depth):
     ovl = RoadVisionEngine(cfg, S, (H, W), device=cuda)
     ovl.step(frames[0], ts[0])  # eager first step (one-time kernel setup)
     run = OverlappedSteps(ovl, [frames[f] for f in range(1, F)], [ts[f] for f in range(1, F)],
-                          depth=depth)
+                          depth=depth, chunk=chunk)
     run.run()
     torch.cuda.synchronize()
     r_seq, r_ovl = seq.results(out_seq), ovl.results(run.outs[-1])
