@@ -123,7 +123,7 @@ def main():
     for f in range(Wm):
         eng.step(frames[f], ts_all[f])
     if not args.no_autotune:  # per-layer conv kernel choice, on real activations
-        eng.autotune(frames[0])
+        eng.autotune(frames[0], reps=int(os.environ.get("RV_AUTOTUNE_REPS", "10")))
     torch.cuda.synchronize()
     lib = _lib.load()
     graphs = runner = None
