@@ -38,6 +38,10 @@ extern "C" {
 /* ABI version (bumped on any signature change) and last-error text. */
 int rv_abi_version(void);
 const char* rv_last_error(void);
+/* Measurement plumbing (no reference counterpart): an empty kernel whose
+ * dispatch marks a point in a rocprofv3 kernel trace (bench.py brackets its
+ * timed region with tags 1 and 2). */
+int rv_trace_marker(int tag, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Preprocess: CLAHEDehaze (src/preprocess/ops/clahe_dehaze.py:13-32,       */
@@ -148,6 +152,12 @@ int rv_yolo_pack(int variant, const float* flat, size_t n, void* host_out, size_
 int rv_yolo_create(int variant, const void* dev_packed, int max_B, int in_h, int in_w,
                    void** handle);
 int rv_yolo_destroy(void* handle);
+/* Handle options.  RV_YOLO_OPT_RAW_UNFUSED (default 1): a forward asked for
+ * raw_out runs the unfused stem, so the P1 map (X0) lands in the workspace
+ * for layer-wise inspection; 0: raw forwards run the production kernel
+ * sequence (fused stem), so raw_out is what the candidate path computed. */
+#define RV_YOLO_OPT_RAW_UNFUSED 1
+int rv_yolo_set_option(void* handle, int opt, int value);
 size_t rv_yolo_ws_bytes(void* handle, int B);
 int rv_yolo_num_anchors(void* handle);
 /* Forward on B letterboxed u8 BGR images (B x in_h x in_w x 3).  raw_out
@@ -196,22 +206,30 @@ int rv_yolo_autotune(void* handle, const uint8_t* lb, int B, void* ws, size_t ws
  * patch kernel, 1: direct-B 1x1 kernel; MR 0 = default
  * heuristic); returns the number of tuned launches (0 before autotuning). */
 int rv_yolo_tuned_config(void* handle, int idx, int* cfg6);
+/* Install a saved configuration (cfg6 as above) for conv launch idx of a
+ * plan with n launches (e.g. reloaded from a file written after an earlier
+ * autotune), so a run can skip the autotuner; an invalid entry falls back to
+ * the default heuristic at launch. */
+int rv_yolo_set_tuned(void* handle, int n, int idx, const int* cfg6);
 
 /* --- Ultralytics non_max_suppression + scale_boxes + class filter
  * (yolo_ultralytics.py:28-53), one workgroup per image. */
 size_t rv_nms_smem_bytes(void);
 /* cand / seg_n: the segmented candidate layout of rv_yolo_forward (nseg
- * segments of 64 rows, cap rows per image).  scale5 = {gain (f32 of the
- * python gain), pad_x, pad_y, clip_w, clip_h}; keep_mask4 (nullable = keep
- * all): 128-bit class mask (classes_keep); out: B x max_det x 6
- * {x1,y1,x2,y2,conf,cls} in score order, out_n[B]; cand_total (nullable):
- * candidates per image; ws: rv_nms_ws_bytes(B) bytes of device workspace. */
+ * segments of 64 rows, cap <= 65536 rows per image).  Every candidate is
+ * sorted (score desc, anchor asc); only the first max_nms of them enter the
+ * greedy pass (Ultralytics non_max_suppression's max_nms = 30000: top
+ * max_nms by score).  scale5 = {gain (f32 of the python gain), pad_x, pad_y,
+ * clip_w, clip_h}; keep_mask4 (nullable = keep all): 128-bit class mask
+ * (classes_keep); out: B x max_det x 6 {x1,y1,x2,y2,conf,cls} in score
+ * order, out_n[B]; cand_total (nullable): candidates per image before
+ * max_nms; ws: rv_nms_ws_bytes(B) bytes of device workspace. */
 int rv_nms_postprocess(const void* cand, const int* seg_n, int B, int cap, int nseg,
-                       float iou, int max_det, float max_wh, const float* scale5,
+                       float iou, int max_det, int max_nms, float max_wh, const float* scale5,
                        const uint32_t* keep_mask4, float* out, int* out_n, int* cand_total,
                        void* ws, size_t ws_bytes, void* stream);
 /* Device workspace rv_nms_postprocess needs for B images (sort keys of
- * images with more than 4096 candidates). */
+ * images with more than 4096 candidates: 65536 x 8 B per image). */
 size_t rv_nms_ws_bytes(int B);
 /* Segments of 64 anchors for a raw prediction with A anchors. */
 int rv_cand_segments(int A);
@@ -240,9 +258,34 @@ int rv_sort_update(void* state_in, void* state_out, int S, int tmax, const float
                    const int* dcount, int dmax, const double* ts, const double* params6,
                    const double* H9, const float* origin2, void* ws, size_t ws_bytes,
                    int* out_id, double* out_dist, double* out_speed, void* stream);
+/* Per-stream capacity report (device outputs, S ints each): live tracks T,
+ * next track id, and the sticky overflow flag -- 1 once a frame had more
+ * live + new tracks than tmax; the new tracks that did not fit were dropped
+ * (their ids were still handed out), so that stream's ids diverge from the
+ * reference's unbounded track list from then on.  next_id_out / overflow_out
+ * are nullable. */
+int rv_sort_stats(const void* state, int S, int* T_out, int* next_id_out, int* overflow_out,
+                  void* stream);
 /* Debug/parity export: per track x[7] (f64) and {id, hits, hit_streak, cls}. */
 int rv_sort_export(const void* state, int S, int tmax, double* x_out, int* meta, int* T_out,
                    void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Result hand-back (yolo_ultralytics.py:44-52 `.cpu().numpy()` + Detection  */
+/* construction; sort_tracker.py:234-247 fills track_id / distance_m /       */
+/* speed_kmh).  One record per step: int32 n[S] (padded to 16 B), then       */
+/* S x dmax rows of 48 B {f32 x1,y1,x2,y2,conf; i32 cls, track_id (-1 =      */
+/* None), pad; f64 distance_m, speed_kmh (NaN = None)}, rows >= n[s] zeroed. */
+/* ------------------------------------------------------------------------ */
+size_t rv_results_bytes(int S, int dmax);
+/* Packs the NMS rows (S x dmax x 6 f32) + counts and the SORT outputs
+ * (track_id / distance_m / speed_kmh, S x dmax; each nullable = None) into
+ * dev_stage (>= rv_results_bytes) and, when host_dst is non-null (pinned
+ * host memory), copies the record there with one stream-ordered
+ * hipMemcpyAsync.  Graph-capturable. */
+int rv_results_handback(const float* dets, const int* det_n, const int* track_id,
+                        const double* distance_m, const double* speed_kmh, int S, int dmax,
+                        void* dev_stage, size_t stage_bytes, void* host_dst, void* stream);
 
 /* --- Standalone pieces of SortTracker.update / GroundProjector, batched over
  * S streams (csrc/track_ops.hip; rv_sort_update fuses the same math). */

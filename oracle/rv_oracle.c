@@ -23,8 +23,11 @@
  * :182-210 and are pinned against vectors produced by the reference code
  * itself (tests/golden/make_golden.py).
  *
- * Build: oracle/Makefile (gcc -O2 -ffp-contract=off; SSE2 scalar floats,
- * no excess precision, no FMA contraction).
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off -fopenmp; SSE2 scalar
+ * floats, no excess precision, no FMA contraction).  The per-pixel loops are
+ * OpenMP-parallel over independent rows / tiles (OMP_NUM_THREADS), as
+ * OpenCV's parallel_for_ is, so the CPU baseline uses the host's cores; the
+ * results do not depend on the thread count.
  */
 #include <math.h>
 #include <stdint.h>
@@ -45,6 +48,7 @@ static int reflect101(int p, int n) {
 
 /* cvtColor COLOR_BGR2YCrCb, 8U */
 void oracle_bgr2ycrcb(const uint8_t* in, uint8_t* out, int n) {
+#pragma omp parallel for schedule(static)
   for (int i = 0; i < n; ++i) {
     int b = in[3 * i], g = in[3 * i + 1], r = in[3 * i + 2];
     int Y = (b * 1868 + g * 9617 + r * 4899 + 8192) >> 14;
@@ -58,6 +62,7 @@ void oracle_bgr2ycrcb(const uint8_t* in, uint8_t* out, int n) {
 
 /* cvtColor COLOR_YCrCb2BGR, 8U */
 void oracle_ycrcb2bgr(const uint8_t* in, uint8_t* out, int n) {
+#pragma omp parallel for schedule(static)
   for (int i = 0; i < n; ++i) {
     int Y = in[3 * i], Cr = in[3 * i + 1], Cb = in[3 * i + 2];
     int b = Y + (((Cb - 128) * 29049 + 8192) >> 14);
@@ -87,9 +92,10 @@ void oracle_clahe_u8c1(const uint8_t* src, uint8_t* dst, int H, int W, int tiles
     if (clip_limit < 1) clip_limit = 1;
   }
   uint8_t* lut = (uint8_t*)malloc((size_t)tiles * tiles * 256);
-  int hist[256];
+#pragma omp parallel for collapse(2) schedule(static)
   for (int ty = 0; ty < tiles; ++ty)
     for (int tx = 0; tx < tiles; ++tx) {
+      int hist[256];
       memset(hist, 0, sizeof(hist));
       for (int r = 0; r < th; ++r) {
         int sy = ty * th + r;
@@ -124,6 +130,7 @@ void oracle_clahe_u8c1(const uint8_t* src, uint8_t* dst, int H, int W, int tiles
       }
     }
   const float inv_tw = 1.0f / tw, inv_th = 1.0f / th;
+#pragma omp parallel for schedule(static)
   for (int y = 0; y < H; ++y) {
     float tyf = y * inv_th - 0.5f;
     int ty1 = (int)floorf(tyf);
@@ -156,9 +163,11 @@ void oracle_clahe_ycrcb(const uint8_t* in, uint8_t* out, int H, int W, int tiles
   uint8_t* y = (uint8_t*)malloc(n);
   uint8_t* y2 = (uint8_t*)malloc(n);
   oracle_bgr2ycrcb(in, ycc, (int)n);
-  for (size_t i = 0; i < n; ++i) y[i] = ycc[3 * i];
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < (long)n; ++i) y[i] = ycc[3 * i];
   oracle_clahe_u8c1(y, y2, H, W, tiles, clip);
-  for (size_t i = 0; i < n; ++i) ycc[3 * i] = y2[i];
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < (long)n; ++i) ycc[3 * i] = y2[i];
   oracle_ycrcb2bgr(ycc, out, (int)n);
   free(ycc);
   free(y);
@@ -173,6 +182,7 @@ static int med3(int a, int b, int c) { return max2(min2(a, b), min2(max2(a, b), 
 
 /* k = 3 fast path: sort each column of 3, median = med3(max(lo), med(mid), min(hi)). */
 static void median3(const uint8_t* in, uint8_t* out, int H, int W) {
+#pragma omp parallel for schedule(static)
   for (int y = 0; y < H; ++y) {
     const uint8_t* r0 = in + (size_t)clampi(y - 1, 0, H - 1) * W * 3;
     const uint8_t* r1 = in + (size_t)y * W * 3;
@@ -200,10 +210,11 @@ void oracle_median_u8c3(const uint8_t* in, uint8_t* out, int H, int W, int k) {
     return;
   }
   const int r = k / 2, n = k * k, rank = n / 2;
-  int w[81];
+#pragma omp parallel for schedule(static)
   for (int y = 0; y < H; ++y)
     for (int x = 0; x < W; ++x)
       for (int c = 0; c < 3; ++c) {
+        int w[81];
         int m = 0;
         for (int dy = -r; dy <= r; ++dy) {
           int sy = clampi(y + dy, 0, H - 1);
@@ -249,6 +260,7 @@ static int round_short(float v) {
 void oracle_letterbox(const uint8_t* in, uint8_t* out, int H, int W, const int* geo) {
   int out_h = geo[0], out_w = geo[1], new_h = geo[2], new_w = geo[3], top = geo[4], left = geo[5];
   double scale_x = 1.0 / ((double)new_w / W), scale_y = 1.0 / ((double)new_h / H);
+#pragma omp parallel for schedule(static)
   for (int oy = 0; oy < out_h; ++oy)
     for (int ox = 0; ox < out_w; ++ox) {
       uint8_t* d = out + ((size_t)oy * out_w + ox) * 3;

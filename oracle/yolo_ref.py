@@ -114,10 +114,36 @@ class YoloRef:
                 w = _bf16(w)
             self.p[n] = (w, b, s, k, act)
         assert off == flat.size, "flat weight size mismatch"
+        self.bn = {}
+
+    @classmethod
+    def from_unfused(cls, variant: int, sd: dict, eps: float = 1e-3) -> "YoloRef":
+        """The UNFUSED Ultralytics network of a state_dict (Conv = conv2d
+        without bias -> BatchNorm2d(eps) in eval mode -> SiLU; the Detect
+        head's last convs plain conv2d + bias): what model.fuse()
+        (yolo_ultralytics.py:16-17) replaces by folded convs."""
+        specs, _ = conv_specs(variant)
+        flat = []
+        for n, ci, co, k, s, act in specs:
+            key = n + ".conv.weight" if n + ".conv.weight" in sd else n + ".weight"
+            flat += [np.asarray(sd[key], np.float32).ravel(),
+                     np.asarray(sd.get(n + ".bias", np.zeros(co)), np.float32).ravel()]
+        m = cls(variant, np.concatenate(flat))
+        for n, ci, co, k, s, act in specs:
+            if n + ".bn.running_var" in sd:
+                t = lambda x: torch.from_numpy(np.asarray(sd[n + x], np.float32))  # noqa: E731
+                m.bn[n] = (t(".bn.running_mean"), t(".bn.running_var"), t(".bn.weight"),
+                           t(".bn.bias"), eps)
+        return m
 
     def conv(self, n, x, res=None):
         w, b, s, k, act = self.p[n]
-        y = F.conv2d(x, w, b, stride=s, padding=k // 2)
+        if n in self.bn:
+            mean, var, g, beta, eps = self.bn[n]
+            y = F.batch_norm(F.conv2d(x, w, None, stride=s, padding=k // 2), mean, var, g, beta,
+                             False, 0.0, eps)
+        else:
+            y = F.conv2d(x, w, b, stride=s, padding=k // 2)
         y = F.silu(y) if act else y
         if res is not None:
             y = res + y

@@ -13,5 +13,16 @@ void set_error(const char* fmt, ...) {
 }
 }  // namespace rv
 
-extern "C" int rv_abi_version(void) { return 2; }
+extern "C" int rv_abi_version(void) { return 3; }
 extern "C" const char* rv_last_error(void) { return rv::g_err; }
+
+// Trace marker: an empty one-wave kernel whose dispatch brackets a region of
+// a rocprofv3 kernel trace (bench.py launches tag 1 right before its timed
+// region and tag 2 right after it; tools/trace_window.py keeps the kernels
+// between them).  No reference counterpart: measurement plumbing only.
+__global__ void rv_trace_marker_kernel(int tag) { (void)tag; }
+
+extern "C" int rv_trace_marker(int tag, void* stream) {
+  rv_trace_marker_kernel<<<1, 64, 0, rv::as_stream(stream)>>>(tag);
+  return rv::launch_status("rv_trace_marker");
+}

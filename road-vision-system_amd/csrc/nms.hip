@@ -17,7 +17,12 @@
 // track stage overlaps the next forward); an image with more candidates is
 // flagged (out_n = -1) and redone by nms_kernel<kSortCap>, which keeps its
 // keys in the caller's workspace (global memory, ~10 KB of LDS) and whose
-// blocks exit at once for every unflagged image.
+// blocks exit at once for every unflagged image.  kSortCap = 65536 covers
+// every slot of the candidate layout (cap <= 65536), so no candidate is ever
+// dropped before the sort.  max_nms: after the sort only the first max_nms
+// keys take part in the greedy pass -- Ultralytics' `if n > max_nms: x =
+// x[x[:, 4].argsort(descending=True)[:max_nms]]` (top max_nms by score; ties
+// resolved in anchor order like the stable sort of the oracle).
 // Greedy: wave 0 walks the sorted list in chunks of 64; each lane tests its
 // candidate against every kept box, builds the 64-bit mask of later chunk
 // members it would suppress, and a uniform scalar loop resolves the chunk.
@@ -25,7 +30,7 @@
 
 namespace rv {
 
-constexpr int kSortCap = 16384;  // candidates per image held in LDS (128 KB)
+constexpr int kSortCap = 65536;  // candidates per image (overflow pass, keys in global memory)
 constexpr int kSortSmall = 4096;  // first pass (32 KB of keys)
 constexpr int kMaxDet = 1024;
 constexpr int kMaxSeg = 1024;    // 64-candidate segments per image (<= 65536 slots)
@@ -70,7 +75,7 @@ template <int CAP>
 __global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand,
                                                    const int* __restrict__ seg_n, int nseg, int cap,
                                                    float max_wh, double iou, int max_det,
-                                                   ScaleArgs sc, const uint32_t* __restrict__ keep4,
+                                                   int max_nms, ScaleArgs sc, const uint32_t* __restrict__ keep4,
                                                    float* __restrict__ out, int* __restrict__ out_n,
                                                    int* __restrict__ cand_total,
                                                    uint64_t* __restrict__ gkeys) {
@@ -119,7 +124,8 @@ __global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand
     if (tid == 0) out_n[b] = -1;
     return;
   }
-  if (n > CAP) n = CAP;  // capacity limit (documented in DESIGN.md)
+  // n <= nseg * 64 <= cap <= kSortCap (checked by the host entry): the
+  // overflow pass sorts every candidate
   int np2 = 1;
   while (np2 < n) np2 <<= 1;
   for (int i = tid; i < np2; i += blockDim.x) keys[i] = ~0ull;
@@ -151,6 +157,8 @@ __global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand
       __syncthreads();
     }
   }
+  // Ultralytics max_nms: only the top max_nms by score enter torchvision nms
+  if (n > max_nms) n = max_nms;
   // greedy NMS on wave 0
   if (tid < 64) {
     const int lane = tid;
@@ -290,7 +298,8 @@ extern "C" size_t rv_nms_smem_bytes(void) { return nms_smem(kSortSmall, kMaxDet)
 extern "C" size_t rv_nms_ws_bytes(int B) { return (size_t)(B > 0 ? B : 0) * kSortCap * 8; }
 
 extern "C" int rv_nms_postprocess(const void* cand, const int* seg_n, int B, int cap, int nseg,
-                                  float iou, int max_det, float max_wh, const float* scale5,
+                                  float iou, int max_det, int max_nms, float max_wh,
+                                  const float* scale5,
                                   const uint32_t* keep_mask4, float* out, int* out_n,
                                   int* cand_total, void* ws, size_t ws_bytes, void* stream) {
   RV_CHECK_ARG(cand && seg_n && out && out_n && scale5, "null pointer");
@@ -298,6 +307,8 @@ extern "C" int rv_nms_postprocess(const void* cand, const int* seg_n, int B, int
   RV_CHECK_ARG(nseg > 0 && nseg <= kMaxSeg && nseg * 64 <= cap,
                "nseg %d: need 0 < nseg <= %d and nseg * 64 <= cap %d", nseg, kMaxSeg, cap);
   RV_CHECK_ARG(max_det > 0 && max_det <= kMaxDet, "max_det %d outside (0, %d]", max_det, kMaxDet);
+  RV_CHECK_ARG(max_nms > 0, "max_nms %d must be positive", max_nms);
+  static_assert(kSortCap >= 65536, "the overflow pass must hold every slot of cap <= 65536");
   RV_CHECK_ARG(ws && ws_bytes >= rv_nms_ws_bytes(B), "workspace %zu B < rv_nms_ws_bytes(%d) = %zu",
                ws_bytes, B, rv_nms_ws_bytes(B));
   if (B == 0) return RV_OK;
@@ -324,13 +335,13 @@ extern "C" int rv_nms_postprocess(const void* cand, const int* seg_n, int B, int
     attr = true;
   }
   nms_kernel<kSortSmall><<<B, 1024, nms_smem(kSortSmall, max_det), as_stream(stream)>>>(
-      (const Cand*)cand, seg_n, nseg, cap, max_wh, (double)iou, max_det, sc, keep_mask4, out,
-      out_n, cand_total, nullptr);
+      (const Cand*)cand, seg_n, nseg, cap, max_wh, (double)iou, max_det, max_nms, sc, keep_mask4,
+      out, out_n, cand_total, nullptr);
   int st = launch_status("rv_nms_postprocess");
   if (st) return st;
   nms_kernel<kSortCap><<<B, 1024, nms_smem(kSortCap, max_det), as_stream(stream)>>>(
-      (const Cand*)cand, seg_n, nseg, cap, max_wh, (double)iou, max_det, sc, keep_mask4, out,
-      out_n, cand_total, (uint64_t*)ws);
+      (const Cand*)cand, seg_n, nseg, cap, max_wh, (double)iou, max_det, max_nms, sc, keep_mask4,
+      out, out_n, cand_total, (uint64_t*)ws);
   return launch_status("rv_nms_postprocess (overflow pass)");
 }
 

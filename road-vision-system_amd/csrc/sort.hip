@@ -501,6 +501,16 @@ __global__ void sort_export_kernel(const StreamHdr* __restrict__ hdr, const Trac
   }
 }
 
+__global__ void sort_stats_kernel(const StreamHdr* __restrict__ hdr, int S, int* __restrict__ T_out,
+                                  int* __restrict__ next_id, int* __restrict__ overflow) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const StreamHdr h = hdr[s];
+  T_out[s] = h.T;
+  if (next_id) next_id[s] = h.next_id;
+  if (overflow) overflow[s] = h.overflow;
+}
+
 }  // namespace rv
 
 using namespace rv;
@@ -596,4 +606,12 @@ extern "C" int rv_sort_export(const void* state, int S, int tmax, double* x_out,
   sort_export_kernel<<<S, 256, 0, as_stream(stream)>>>(
       (const StreamHdr*)state, (const Track*)((const uint8_t*)state + hb), tmax, x_out, meta, T_out);
   return launch_status("rv_sort_export");
+}
+
+extern "C" int rv_sort_stats(const void* state, int S, int* T_out, int* next_id_out,
+                             int* overflow_out, void* stream) {
+  RV_CHECK_ARG(state && T_out && S > 0, "bad args");
+  sort_stats_kernel<<<ceil_div(S, 256), 256, 0, as_stream(stream)>>>(
+      (const StreamHdr*)state, S, T_out, next_id_out, overflow_out);
+  return launch_status("rv_sort_stats");
 }

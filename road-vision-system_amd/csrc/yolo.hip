@@ -214,6 +214,9 @@ struct Model {
     }
   }
   int max_B = 0, H = 0, W = 0;
+  // RV_YOLO_OPT_RAW_UNFUSED: forwards that return the raw prediction run the
+  // unfused stem, so every activation (X0 included) is in the workspace
+  int raw_unfused = 1;
   std::vector<Buf> bufs;
   int nA = 0;
   int map_h[6], map_w[6];  // stride 2^i maps
@@ -594,6 +597,19 @@ extern "C" int rv_yolo_destroy(void* h) {
   return RV_OK;
 }
 
+extern "C" int rv_yolo_set_option(void* h, int opt, int value) {
+  RV_CHECK_ARG(h, "null handle");
+  Model* M = (Model*)h;
+  switch (opt) {
+    case RV_YOLO_OPT_RAW_UNFUSED:
+      M->raw_unfused = value != 0;
+      return RV_OK;
+    default:
+      set_error("unknown yolo option %d", opt);
+      return RV_EINVAL;
+  }
+}
+
 extern "C" size_t rv_yolo_ws_bytes(void* h, int B) {
   if (!h || B <= 0) return 0;
   return ((Model*)h)->ws_bytes(B);
@@ -636,11 +652,12 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   // backbone
   const ConvSpec& c0 = M->def.convs[0];
   // conv0 + model.1 fused (the P1 map stays in LDS) unless the caller asked
-  // for the raw prediction (parity / debug forwards keep every activation
-  // in the workspace) or RV_FUSE_STEM=0
+  // for the raw prediction with RV_YOLO_OPT_RAW_UNFUSED set (layer parity
+  // forwards keep every activation in the workspace) or RV_FUSE_STEM=0
   static const bool stem_env = !getenv("RV_FUSE_STEM") || atoi(getenv("RV_FUSE_STEM")) != 0;
   const int i1 = M->def.find("model.1");
-  const bool fuse_stem = stem_env && !raw_out && c0.cout == 16 && v.c2 == 32 && i1 >= 0;
+  const bool fuse_stem =
+      stem_env && !(raw_out && M->raw_unfused) && c0.cout == 16 && v.c2 == 32 && i1 >= 0;
   int st;
   if (fuse_stem) {
     const ConvSpec& c1 = M->def.convs[i1];
@@ -991,6 +1008,18 @@ extern "C" int rv_yolo_tuned_config(void* h, int idx, int* cfg6) {
     cfg6[5] = c.kind;
   }
   return (int)M->tuned.size();
+}
+
+// Install a configuration for conv launch idx (saved from rv_yolo_tuned_config
+// of an earlier autotune of the same plan): n = number of launches of the
+// plan (resizes the table; entries not set keep the default heuristic).
+// Invalid configurations fall back to the default at launch (conv_cfg_ok).
+extern "C" int rv_yolo_set_tuned(void* h, int n, int idx, const int* cfg6) {
+  RV_CHECK_ARG(h && cfg6 && n > 0 && idx >= 0 && idx < n, "bad args");
+  Model* M = (Model*)h;
+  if ((int)M->tuned.size() != n) M->tuned.assign(n, ConvCfg{0, 0, 0, 0, 0});
+  M->tuned[idx] = ConvCfg{cfg6[0], cfg6[1], cfg6[2], cfg6[3], cfg6[4], cfg6[5]};
+  return RV_OK;
 }
 
 // Algorithmic HBM bytes of each conv launch of the profiled forwards (same

@@ -48,6 +48,10 @@ _SIGS = {
     "rv_clahe_median_letterbox_fits": (c_int, [c_int, c_int, c_int, c_int, POINTER(c_int)]),
     "rv_gray_span_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                 c_void_p]),
+    # result hand-back
+    "rv_results_bytes": (c_size_t, [c_int, c_int]),
+    "rv_results_handback": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                    c_void_p, c_size_t, c_void_p, c_void_p]),
     # standalone tracker / geometry pieces
     "rv_iou_matrix_batched": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                       c_int, c_int, c_void_p]),
@@ -75,6 +79,7 @@ _SIGS = {
     "rv_yolo_pack": (c_int, [c_int, c_void_p, c_size_t, c_void_p, c_size_t]),
     "rv_yolo_create": (c_int, [c_int, c_void_p, c_int, c_int, c_int, POINTER(c_void_p)]),
     "rv_yolo_destroy": (c_int, [c_void_p]),
+    "rv_yolo_set_option": (c_int, [c_void_p, c_int, c_int]),
     "rv_yolo_ws_bytes": (c_size_t, [c_void_p, c_int]),
     "rv_yolo_num_anchors": (c_int, [c_void_p]),
     "rv_yolo_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_float,
@@ -88,9 +93,11 @@ _SIGS = {
     "rv_yolo_autotune": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_int, c_int,
                                  POINTER(c_int), c_void_p]),
     "rv_yolo_tuned_config": (c_int, [c_void_p, c_int, POINTER(c_int)]),
+    "rv_yolo_set_tuned": (c_int, [c_void_p, c_int, c_int, POINTER(c_int)]),
+    "rv_trace_marker": (c_int, [c_int, c_void_p]),
     "rv_nms_smem_bytes": (c_size_t, []),
     "rv_nms_postprocess": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int,
-                                   c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_size_t, c_void_p]),
     "rv_nms_ws_bytes": (c_size_t, [c_int]),
     "rv_cand_segments": (c_int, [c_int]),
@@ -104,6 +111,7 @@ _SIGS = {
     "rv_sort_update": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rv_sort_stats": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rv_sort_export": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 

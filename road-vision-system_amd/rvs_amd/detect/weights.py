@@ -4,10 +4,22 @@ The conv list (names, shapes, order) comes from the native plan in
 csrc/yolo.hip (rv_yolo_conv_info) -- Ultralytics state_dict order with BN
 fused.  Real checkpoints are not available in this environment
 (.MISSING_LARGE_BLOBS:1 lists yolov8n.pt; there is no network), so weights are
-either loaded from a local .npz / .safetensors of fused tensors keyed by the
-Ultralytics module names ("model.2.m.0.cv1.weight" / ".bias"), or generated
-synthetically from a seed (He-normal, calibrated so a 1080p frame yields a few
-hundred NMS candidates like a trained model on a road scene).
+either loaded from a local Ultralytics state_dict (load_weights: .safetensors,
+.npz, or a tensors-only torch file read with weights_only=True -- never a
+pickle), or generated synthetically from a seed.
+
+load_weights accepts the Ultralytics DetectionModel state_dict keys as they
+are before and after ``model.fuse()`` (the reference calls it,
+src/detect/yolo_ultralytics.py:16-17):
+  * unfused Conv blocks: ``model.N[...].conv.weight`` + ``.bn.weight / .bn.bias
+    / .bn.running_mean / .bn.running_var`` -- folded here exactly as
+    ultralytics.utils.torch_utils.fuse_conv_and_bn does (BatchNorm2d eps =
+    1e-3, set by initialize_weights), in float32;
+  * fused Conv blocks: ``model.N[...].conv.weight`` + ``.conv.bias``;
+  * the Detect head's plain 1x1 convs: ``model.22.cv2.i.2.weight / .bias``;
+  * the plan's own names (``model.2.m.0.cv1.weight / .bias``, round-1 files).
+The DFL conv (``model.22.dfl.conv.weight``, a fixed arange) and
+``num_batches_tracked`` are ignored.
 """
 from __future__ import annotations
 
@@ -77,20 +89,84 @@ def synthetic_weights(variant: int, seed: int = 0) -> np.ndarray:
     return np.concatenate(parts).astype(np.float32)
 
 
-def load_weights(path: str, variant: int) -> np.ndarray:
-    """Flat f32 array from a local .npz / .safetensors of fused tensors."""
+BN_EPS = 1e-3  # ultralytics.nn.tasks.initialize_weights: BatchNorm2d.eps = 1e-3
+
+
+def fold_bn(w: np.ndarray, gamma: np.ndarray, beta: np.ndarray, mean: np.ndarray,
+            var: np.ndarray, bias=None, eps: float = BN_EPS):
+    """ultralytics.utils.torch_utils.fuse_conv_and_bn in float32 torch ops:
+    w_bn = diag(gamma / sqrt(eps + var)); W = w_bn @ w; b = w_bn @ b_conv +
+    (beta - gamma * mean / sqrt(var + eps)).  torch's own sqrt / div / mul
+    are used (torch's CPU sqrt is not always the correctly rounded one, and
+    the reference folds with it); the diagonal matmuls are evaluated as the
+    exact per-row products they denote (a BLAS sgemm of a diagonal matrix
+    returns some of them 1 ulp off, platform-dependently)."""
+    import torch
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32))  # noqa: E731
+    w, gamma, beta, mean, var = t(w), t(gamma), t(beta), t(mean), t(var)
+    scale = gamma.div(torch.sqrt(eps + var))
+    wf = scale.view(-1, *([1] * (w.dim() - 1))) * w
+    b_conv = torch.zeros_like(beta) if bias is None else t(bias)
+    b_bn = beta - gamma.mul(mean).div(torch.sqrt(var + eps))
+    return wf.numpy(), (scale * b_conv + b_bn).numpy()
+
+
+def read_state_dict(path: str) -> Dict[str, np.ndarray]:
+    """Tensors of a local checkpoint, with loaders that execute nothing
+    from the file: .safetensors, .npz (allow_pickle=False), or a torch file
+    of plain tensors (torch.load(weights_only=True))."""
     if path.endswith(".safetensors"):
         from safetensors.numpy import load_file
-        tensors: Dict[str, np.ndarray] = load_file(path)
-    else:
+        return dict(load_file(path))
+    if path.endswith(".npz"):
         with np.load(path, allow_pickle=False) as z:
-            tensors = {k: z[k] for k in z.files}
+            return {k: z[k] for k in z.files}
+    import torch
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    if not isinstance(sd, dict):
+        raise ValueError(f"{path}: expected a state_dict of tensors (save model.state_dict())")
+    return {k: v.detach().float().numpy() if hasattr(v, "detach") else np.asarray(v)
+            for k, v in sd.items()}
+
+
+def _strip_prefix(t: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
+    # YOLO(...).state_dict() nests the DetectionModel under "model."
+    if any(k.startswith("model.model.") for k in t):
+        t = {k[len("model."):]: v for k, v in t.items() if k.startswith("model.")}
+    return t
+
+
+def flat_from_state_dict(tensors: Dict[str, np.ndarray], variant: int) -> np.ndarray:
+    """Flat f32 weights (the plan's conv order) from an Ultralytics
+    DetectionModel state_dict, fused or not (see the module docstring)."""
+    t = _strip_prefix(tensors)
     parts = []
     for name, cin, cout, k, s, act in conv_list(variant):
-        w = np.asarray(tensors[name + ".weight"], np.float32).reshape(cout, cin, k, k)
-        b = np.asarray(tensors[name + ".bias"], np.float32).reshape(cout)
-        parts += [w.ravel(), b]
-    return np.concatenate(parts)
+        shape = (cout, cin, k, k)
+        if name + ".conv.weight" in t:  # Conv block (conv + bn + SiLU)
+            w = np.asarray(t[name + ".conv.weight"], np.float32).reshape(shape)
+            if name + ".bn.running_var" in t:
+                w, b = fold_bn(w, t[name + ".bn.weight"], t[name + ".bn.bias"],
+                               t[name + ".bn.running_mean"], t[name + ".bn.running_var"],
+                               t.get(name + ".conv.bias"))
+            elif name + ".conv.bias" in t:
+                b = np.asarray(t[name + ".conv.bias"], np.float32)
+            else:
+                raise KeyError(f"{name}: neither .bn.* nor .conv.bias in the state_dict")
+        elif name + ".weight" in t:  # Detect's plain nn.Conv2d / the plan's own names
+            w = np.asarray(t[name + ".weight"], np.float32).reshape(shape)
+            b = np.asarray(t[name + ".bias"], np.float32)
+        else:
+            raise KeyError(f"{name}: no weights in the state_dict "
+                           f"(expected {name}.conv.weight or {name}.weight)")
+        parts += [w.ravel(), b.reshape(cout)]
+    return np.concatenate(parts).astype(np.float32)
+
+
+def load_weights(path: str, variant: int) -> np.ndarray:
+    """Flat f32 array from a local Ultralytics checkpoint (state_dict keys,
+    fused or unfused; see read_state_dict for the accepted formats)."""
+    return flat_from_state_dict(read_state_dict(path), variant)
 
 
 def pack(variant: int, flat: np.ndarray) -> np.ndarray:
@@ -102,3 +178,23 @@ def pack(variant: int, flat: np.ndarray) -> np.ndarray:
     _lib.check(lib.rv_yolo_pack(variant, flat.ctypes.data, flat.size, out.ctypes.data, nbytes),
                "rv_yolo_pack")
     return out
+
+
+def weights_from_config(det_cfg: dict, variant: int) -> np.ndarray:
+    """The detector's weights for a detect config (default.yaml:38-45 keys):
+    ``weights: <path>`` loads a local Ultralytics state_dict (load_weights);
+    ``weights: synthetic`` opts in to the seeded synthetic weights (``seed``).
+    With no ``weights`` key the synthetic weights are used too, with a
+    warning: the reference's YOLO(model) loads the real checkpoint, and a
+    production run must not silently detect with random weights."""
+    import warnings
+    w = det_cfg.get("weights")
+    seed = int(det_cfg.get("seed", 0))
+    if w and str(w).lower() != "synthetic":
+        return load_weights(str(w), variant)
+    if not w:
+        warnings.warn(f"detect.model={det_cfg.get('model', 'yolov8n.pt')!r} but no detect.weights "
+                      "file is configured: using seeded SYNTHETIC weights (set detect.weights to "
+                      "a local state_dict, or to 'synthetic' to silence this)", RuntimeWarning,
+                      stacklevel=2)
+    return synthetic_weights(variant, seed=seed)

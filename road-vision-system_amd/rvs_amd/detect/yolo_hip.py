@@ -22,7 +22,7 @@ from .. import _lib, kernels
 from .._lib import call, ptr, stream_ptr
 from .base import Detector
 from .types import Detection
-from .weights import COCO80, load_weights, pack, synthetic_weights, variant_of
+from .weights import COCO80, pack, variant_of, weights_from_config
 
 CAND_BYTES = 32
 
@@ -53,13 +53,14 @@ class YoloEngine:
     def __init__(self, variant: int, flat_weights: np.ndarray, max_batch: int, frame_hw,
                  imgsz: int = 640, stride: int = 32, conf: float = 0.25, iou: float = 0.7,
                  max_det: int = 100, classes_keep: Sequence[int] = (), max_wh: float = 7680.0,
-                 device="cuda"):
+                 max_nms: int = 30000, device="cuda"):
         self.device = torch.device(device)
         self.variant = variant
         self.H, self.W = int(frame_hw[0]), int(frame_hw[1])
         self.max_batch = int(max_batch)
         self.conf, self.iou, self.max_det, self.max_wh = float(conf), float(iou), int(max_det), \
             float(max_wh)
+        self.max_nms = int(max_nms)  # Ultralytics non_max_suppression default
         self.geo = kernels.letterbox_geometry(self.H, self.W, imgsz, stride)
         self.in_h, self.in_w = self.geo[0], self.geo[1]
         self.packed = torch.from_numpy(pack(variant, flat_weights)).to(self.device)
@@ -109,6 +110,12 @@ class YoloEngine:
         except Exception:
             pass
 
+    def set_raw_fused(self, fused: bool) -> None:
+        """Raw forwards run the production kernel sequence (fused stem) when
+        True, so forward_raw(raw) reproduces the candidate path's prediction
+        exactly; False (default) keeps every activation for layer tests."""
+        call("rv_yolo_set_option", self._h, 1, 0 if fused else 1)
+
     def letterbox(self, frames: torch.Tensor, slot: int = 0) -> torch.Tensor:
         B = frames.shape[0]
         return kernels.letterbox(frames, self.geo, out=self.lb[slot][:B])
@@ -149,10 +156,18 @@ class YoloEngine:
             out.append(tuple(c))
         return out
 
+    def load_tuned(self, cfgs) -> None:
+        """Install saved per-launch configurations (tuned_configs() of an
+        earlier autotune of the same plan) instead of autotuning."""
+        n = len(cfgs)
+        for i, c in enumerate(cfgs):
+            call("rv_yolo_set_tuned", self._h, n, i, _lib.int_array(c))
+
     def nms(self, B: int, slot: int = 0):
         """NMS + scale_boxes + class filter of candidate slot `slot`."""
         call("rv_nms_postprocess", ptr(self.cand[slot]), ptr(self.seg_n[slot]), B, self.cap,
-             self._nseg_cur, self.iou, self.max_det, self.max_wh, ptr(self.scale5), ptr(self.keep),
+             self._nseg_cur, self.iou, self.max_det, self.max_nms, self.max_wh, ptr(self.scale5),
+             ptr(self.keep),
              ptr(self.dets), ptr(self.det_n), ptr(self.cand_n), ptr(self.nms_ws),
              self.nms_ws.numel(), stream_ptr())
         return self.dets[:B], self.det_n[:B]
@@ -208,9 +223,7 @@ class YOLOHip(Detector):
         if not torch.cuda.is_available():
             raise RuntimeError("YOLOHip needs an MI355X (HIP device); there is no CPU fallback")
         self.variant = variant_of(cfg.get("model", "yolov8n.pt"))
-        wpath = cfg.get("weights")
-        self.flat = (load_weights(wpath, self.variant) if wpath else
-                     synthetic_weights(self.variant, seed=int(cfg.get("seed", 0))))
+        self.flat = weights_from_config(cfg, self.variant)
         self.conf = float(cfg.get("conf_thres", 0.25))
         self.iou = float(cfg.get("iou_thres", 0.7))
         self.max_det = int(cfg.get("max_det", 100))

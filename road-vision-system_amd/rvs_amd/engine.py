@@ -11,6 +11,7 @@ step.  ``results()`` converts one step's device outputs into the reference's
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Dict, List, Optional
 
@@ -19,9 +20,10 @@ import torch
 
 from .config import load_config
 from .detect.types import Detection
-from .detect.weights import COCO80, load_weights, synthetic_weights, variant_of
+from .detect.weights import COCO80, variant_of, weights_from_config
 from .detect.yolo_hip import YoloEngine
 from .geometry import GroundProjector, build_projector
+from .handback import Record, handback, to_detections
 from .preprocess import PreprocessPipeline
 from .track.sort_hip import MultiStreamSort
 
@@ -39,9 +41,7 @@ class RoadVisionEngine:
         det_cfg = cfg.get("detect", {}) or {}
         self.variant = variant_of(det_cfg.get("model", "yolov8n.pt"))
         if weights is None:
-            wpath = det_cfg.get("weights")
-            weights = load_weights(wpath, self.variant) if wpath else \
-                synthetic_weights(self.variant, seed=int(det_cfg.get("seed", 0)))
+            weights = weights_from_config(det_cfg, self.variant)
         self.detector = YoloEngine(
             self.variant, weights, self.S, (self.H, self.W), imgsz=int(det_cfg.get("imgsz", 640)),
             conf=float(det_cfg.get("conf_thres", 0.25)), iou=float(det_cfg.get("iou_thres", 0.7)),
@@ -58,6 +58,9 @@ class RoadVisionEngine:
         self.tracker.set_projector(projector)
         self.proc = torch.empty((self.S, self.H, self.W, 3), dtype=torch.uint8, device=self.device)
         self.names = COCO80
+        # result hand-back: device staging buffer + the pinned host record of step()
+        self.record = Record(self.S, self.detector.max_det, self.device)
+        self.rec_stage = torch.empty(self.record.nbytes, dtype=torch.uint8, device=self.device)
         # default chain: CLAHE + median + the detector's LetterBox in one pass
         self.fused_letterbox = self.pipeline.letterbox_fusable(self.H, self.W, self.detector.geo)
 
@@ -86,17 +89,24 @@ class RoadVisionEngine:
         _, lb = self.preprocess_stage(frames)
         return self.detector.autotune(lb, reps=reps, verify=verify)
 
-    def track_stage(self, ts: torch.Tensor, slot: int = 0) -> Dict[str, torch.Tensor]:
-        """NMS of candidate slot `slot` + SORT/geometry (main_preview.py:99-109)."""
+    def track_stage(self, ts: torch.Tensor, slot: int = 0,
+                    record: Optional[Record] = None) -> Dict[str, torch.Tensor]:
+        """NMS of candidate slot `slot` + SORT/geometry (main_preview.py:99-109),
+        then the hand-back of the results into `record` (pinned host)."""
         dets, det_n = self.detector.nms(ts.shape[0], slot)
         tid, dist, spd = self.tracker.update(dets, det_n, ts)
-        return {"dets": dets, "det_n": det_n, "track_id": tid, "distance_m": dist,
-                "speed_kmh": spd}
+        out = {"dets": dets, "det_n": det_n, "track_id": tid, "distance_m": dist,
+               "speed_kmh": spd}
+        if record is not None:
+            handback(dets, det_n, tid, dist, spd, self.rec_stage, record.host)
+            out["record"] = record
+        return out
 
     def step(self, frames: torch.Tensor, ts: torch.Tensor) -> Dict[str, torch.Tensor]:
-        """frames (S,H,W,3) u8 on device, ts (S,) f64 on device."""
+        """frames (S,H,W,3) u8 on device, ts (S,) f64 on device.  The step's
+        results end in self.record (pinned host), read by results()."""
         proc = self.detect_stage(frames, 0)
-        out = self.track_stage(ts, 0)
+        out = self.track_stage(ts, 0, self.record)
         out["proc"] = proc
         return out
 
@@ -115,6 +125,12 @@ class RoadVisionEngine:
         return g, out
 
     def results(self, out: Dict[str, torch.Tensor]) -> List[List[Detection]]:
+        """The reference's Detection lists of one step: from its host record
+        (synchronises the device first), or from the device tensors."""
+        if "record" in out:
+            torch.cuda.synchronize(self.device)
+            n, rows = out["record"].arrays()
+            return to_detections(n, rows, self.names)
         d = out["dets"].cpu().numpy()
         n = out["det_n"].cpu().numpy()
         tid = out["track_id"].cpu().numpy()
@@ -134,6 +150,10 @@ class RoadVisionEngine:
             res.append(lst)
         return res
 
+    def track_stats(self) -> Dict[str, np.ndarray]:
+        """Per-stream SORT capacity report (MultiStreamSort.stats)."""
+        return self.tracker.stats()
+
     def close(self):
         self.detector.close()
 
@@ -151,26 +171,42 @@ class OverlappedSteps:
     letterbox batch and the NMS candidates are double-buffered by step
     parity); with `depth=2` it runs  [T(j-1) || P(j)] -> Y(j).  A prologue /
     epilogue graph fills and drains the pipeline.  Replayed in order, the K
-    steps give the same results as K step() calls (tests/test_engine_gpu.py)."""
+    steps give the same results as K step() calls (tests/test_engine_gpu.py).
+
+    Each step's T stage ends with the result hand-back into that step's own
+    pinned host record (outs[k]["record"]), so every outs[k] holds step k's
+    detections and track ids after run(); outs[k]["proc"] is step k's proc
+    batch.  The device tensors of the NMS / SORT outputs are shared by all
+    steps and are not kept in outs."""
 
     def __init__(self, eng: "RoadVisionEngine", frames, ts, depth: int = 2,
-                 chunk: Optional[int] = None):
+                 chunk: Optional[int] = None, capture: bool = True):
+        """capture=False runs the same multi-stream schedule eagerly, right
+        here (no graphs; run() is then a no-op): bench.py's per-launch conv
+        timing uses it, since HIP events recorded inside captured graphs
+        do not time on ROCm 7.2 (measured: zero elapsed)."""
         self.eng = eng
+        ctx = (lambda g: torch.cuda.graph(g)) if capture else (lambda g: contextlib.nullcontext())
         K = len(frames)
         dev = eng.device
         side_t, side_p = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
         self.graphs = []
         self.outs = []
+        self.records = [Record(eng.S, eng.detector.max_det, dev) for _ in range(K)]
         procs = {}
+
+        def track(j):
+            o = eng.track_stage(ts[j], j % 2, self.records[j])
+            return {"record": o["record"]}
         if depth == 2:
             for j in range(K + 1):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                g = torch.cuda.CUDAGraph() if capture else None
+                with ctx(g):
                     cur = torch.cuda.current_stream()
                     if j > 0:
                         side_t.wait_stream(cur)
                         with torch.cuda.stream(side_t):
-                            out = eng.track_stage(ts[j - 1], (j - 1) % 2)
+                            out = track(j - 1)
                     if j < K:
                         procs[j], lb = eng.preprocess_stage(frames[j])
                     if j > 0:
@@ -179,7 +215,8 @@ class OverlappedSteps:
                         self.outs.append(out)
                     if j < K:
                         eng.yolo_stage(lb, j % 2)
-                self.graphs.append(g)
+                if capture:
+                    self.graphs.append(g)
             return
         lbs = {}
         # steps per captured graph (`chunk`, RV_GRAPH_CHUNK): consecutive
@@ -191,8 +228,8 @@ class OverlappedSteps:
         js = list(range(-1, K + 1))
         size = len(js) if chunk <= 0 else chunk
         for c0 in range(0, len(js), size):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            g = torch.cuda.CUDAGraph() if capture else None
+            with ctx(g):
                 for j in js[c0:c0 + size]:
                     cur = torch.cuda.current_stream()
                     side_t.wait_stream(cur)
@@ -203,7 +240,7 @@ class OverlappedSteps:
                                                                             (j + 1) % 2)
                     if j >= 1:  # T(j-1) from candidate slot (j-1) % 2
                         with torch.cuda.stream(side_t):
-                            out = eng.track_stage(ts[j - 1], (j - 1) % 2)
+                            out = track(j - 1)
                     if 0 <= j < K:  # Y(j)
                         eng.yolo_stage(lbs.pop(j), j % 2)
                     cur.wait_stream(side_p)
@@ -211,7 +248,8 @@ class OverlappedSteps:
                     if j >= 1:
                         out["proc"] = procs.pop(j - 1)
                         self.outs.append(out)
-            self.graphs.append(g)
+            if capture:
+                self.graphs.append(g)
 
     def run(self):
         for g in self.graphs:

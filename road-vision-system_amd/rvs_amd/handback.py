@@ -1,0 +1,77 @@
+"""Host side of the result hand-back (rv_results_handback).
+
+The reference's per-frame path ends on the host: YOLOUltralytics.infer copies
+``boxes.xyxy / conf / cls`` with ``.cpu().numpy()`` and builds ``Detection``
+objects (src/detect/yolo_ultralytics.py:44-52), and SortTracker.update fills
+``track_id / distance_m / speed_kmh`` on them (sort_tracker.py:234-247).  On
+the device a step's outputs are packed into one record and copied to pinned
+host memory by the step itself (csrc/results.hip); this module reads that
+record and materialises the reference's ``List[Detection]`` per stream.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .detect.types import Detection
+
+ROW = np.dtype([("x1", "<f4"), ("y1", "<f4"), ("x2", "<f4"), ("y2", "<f4"), ("conf", "<f4"),
+                ("cls", "<i4"), ("track_id", "<i4"), ("pad", "<i4"), ("dist", "<f8"),
+                ("speed", "<f8")])
+assert ROW.itemsize == 48
+
+
+def record_bytes(S: int, dmax: int) -> int:
+    return int(_lib.load().rv_results_bytes(S, dmax))
+
+
+def _header(S: int) -> int:
+    return (S * 4 + 15) & ~15
+
+
+class Record:
+    """A pinned host record plus its device staging buffer."""
+
+    def __init__(self, S: int, dmax: int, device, host: bool = True):
+        self.S, self.dmax = int(S), int(dmax)
+        self.nbytes = record_bytes(self.S, self.dmax)
+        self.host = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True) if host else None
+
+    def arrays(self):
+        """(counts (S,), rows (S, dmax) structured) views of the host record.
+        The caller must have synchronised the stream that filled it."""
+        buf = self.host.numpy()
+        n = buf[:4 * self.S].view(np.int32)
+        rows = buf[_header(self.S):self.nbytes].view(ROW).reshape(self.S, self.dmax)
+        return n, rows
+
+
+def handback(dets: torch.Tensor, det_n: torch.Tensor, track_id, distance_m, speed_kmh,
+             stage: torch.Tensor, host: torch.Tensor = None) -> None:
+    """Pack one step's device outputs into `stage` and (if `host` is given)
+    copy them to the pinned host record, stream-ordered on the current
+    stream (capturable into a HIP graph)."""
+    S, dmax = dets.shape[0], dets.shape[1]
+    _lib.call("rv_results_handback", _lib.ptr(dets), _lib.ptr(det_n), _lib.ptr(track_id),
+              _lib.ptr(distance_m), _lib.ptr(speed_kmh), S, dmax, _lib.ptr(stage),
+              stage.numel(), _lib.ptr(host), _lib.stream_ptr())
+
+
+def to_detections(n: np.ndarray, rows: np.ndarray, names: Sequence[str]) -> List[List[Detection]]:
+    """The reference's Detection lists (yolo_ultralytics.py:48-52 fields plus
+    the tracker's track_id / distance_m / speed_kmh; NaN / -1 -> None)."""
+    out = []
+    nn = len(names)
+    for s in range(rows.shape[0]):
+        lst = []
+        for x1, y1, x2, y2, conf, k, tid, _, dist, spd in rows[s, :int(n[s])].tolist():
+            lst.append(Detection(x1, y1, x2, y2, conf, k, str(names[k]) if 0 <= k < nn else str(k),
+                                 None if tid < 0 else tid,
+                                 None if math.isnan(dist) else dist,
+                                 None if math.isnan(spd) else spd))
+        out.append(lst)
+    return out

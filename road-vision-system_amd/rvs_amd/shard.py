@@ -8,7 +8,9 @@ barrier and a max over ranks of the timed region (weak scaling).
 """
 from __future__ import annotations
 
-from typing import List
+import os
+import time
+from typing import Callable, List, Optional, Tuple
 
 import torch
 
@@ -41,3 +43,44 @@ def max_over_ranks(value: float, device=None) -> float:
 def job_throughput(frames_per_rank: int, world: int, elapsed_max_s: float) -> float:
     """Whole-job frames/s: every rank's frames over the slowest rank's time."""
     return frames_per_rank * world / elapsed_max_s
+
+
+def init_from_env(backend: str = "nccl") -> Tuple[int, int, int]:
+    """(rank, world, local_rank) from the torchrun environment; joins the
+    process group when world > 1 (nccl = RCCL on ROCm, bound to the local
+    GPU; gloo for CPU rehearsals).  No group for a single process."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not torch.distributed.is_initialized():
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            torch.distributed.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(backend)
+    return rank, world, local
+
+
+def _barrier() -> None:
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        torch.distributed.barrier()
+
+
+def timed_job(run: Callable[[], None], sync: Callable[[], None], units_per_rank: int,
+              device=None) -> dict:
+    """The timed region every rank runs: barrier + device sync, `run()` (the
+    K steps), device sync, barrier; the elapsed time is reduced with a MAX
+    over ranks and the whole-job rate is all ranks' units over that time.
+    Returns {"local_s", "elapsed_s" (max over ranks), "value"}."""
+    world = torch.distributed.get_world_size() if (
+        torch.distributed.is_available() and torch.distributed.is_initialized()) else 1
+    _barrier()
+    sync()
+    t0 = time.perf_counter()
+    run()
+    sync()
+    local = time.perf_counter() - t0
+    _barrier()
+    elapsed = max_over_ranks(local, device)
+    return {"local_s": local, "elapsed_s": elapsed,
+            "value": job_throughput(units_per_rank, world, elapsed)}

@@ -78,6 +78,29 @@ class MultiStreamSort:
         """Tracker.update over all S streams at once (module update_many)."""
         return update_many(self, streams, timestamps)
 
+    def stats(self) -> dict:
+        """Per-stream capacity report (rv_sort_stats), host numpy arrays:
+        T (live tracks), next_id, overflow (1 once the stream had more live +
+        new tracks than tmax: the tracks that did not fit were dropped and the
+        stream's ids diverge from the reference's unbounded list from then
+        on).  Synchronises the device."""
+        T = torch.empty(self.S, dtype=torch.int32, device=self.device)
+        nid = torch.empty(self.S, dtype=torch.int32, device=self.device)
+        ovf = torch.empty(self.S, dtype=torch.int32, device=self.device)
+        call("rv_sort_stats", ptr(self.state[self.cur]), self.S, ptr(T), ptr(nid), ptr(ovf),
+             stream_ptr())
+        return {"T": T.cpu().numpy(), "next_id": nid.cpu().numpy(), "overflow": ovf.cpu().numpy()}
+
+    def check_capacity(self) -> None:
+        """Raise if any stream overflowed tmax (the results are then no longer
+        the reference's); call after a run, outside graph capture."""
+        st = self.stats()
+        bad = np.nonzero(st["overflow"])[0]
+        if len(bad):
+            raise _lib.RVError(f"SORT capacity: streams {bad.tolist()} exceeded tmax={self.tmax} "
+                               f"live tracks (max T now {int(st['T'].max())}); construct with a "
+                               "larger tmax")
+
     def export(self):
         """Host copy of every stream's tracks: (T[S], x[S,tmax,7], meta[S,tmax,4])."""
         x = torch.empty((self.S, self.tmax, 7), dtype=torch.float64, device=self.device)

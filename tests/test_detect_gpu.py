@@ -96,18 +96,21 @@ def _raw_from_boxes(boxes, scores, cls, A, nc=80):
 
 
 # "overflow": more candidates than the first NMS pass sorts in LDS (4096), so
-# the image is redone by the 16384-key overflow pass
-@pytest.mark.parametrize("case", ["ties", "dense", "empty", "many", "overflow", "maxdet", "classes"])
+# the image is redone by the overflow pass (keys in global memory);
+# "maxnms": Ultralytics' max_nms cut (top max_nms by score) at a small max_nms
+@pytest.mark.parametrize("case", ["ties", "dense", "empty", "many", "overflow", "maxdet", "classes",
+                                  "maxnms"])
 def test_nms_edge_cases(cuda, case):
     rng = np.random.default_rng(hash(case) % 2**32)
     A = 5040
+    max_nms = 64 if case == "maxnms" else 30000
     eng, _ = _engine(1080, 1920, 1, cuda, max_det=100 if case != "maxdet" else 7,
-                     classes_keep=[2, 7] if case == "classes" else ())
+                     classes_keep=[2, 7] if case == "classes" else (), max_nms=max_nms)
     if case == "empty":
         boxes, scores, cls = np.zeros((0, 4)), np.zeros(0), np.zeros(0, int)
     else:
         n = {"ties": 300, "dense": 400, "many": 4000, "overflow": 5000, "maxdet": 200,
-             "classes": 500}[case]
+             "classes": 500, "maxnms": 400}[case]
         xy = rng.uniform(0, 600, (n, 2))
         wh = rng.uniform(10, 120, (n, 2)) if case != "dense" else rng.uniform(200, 260, (n, 2))
         boxes = np.concatenate([xy, xy + wh], 1)
@@ -121,8 +124,48 @@ def test_nms_edge_cases(cuda, case):
     raw = _raw_from_boxes(boxes, scores, cls, A)
     dets, n_ = eng.nms_from_raw(torch.from_numpy(raw).to(cuda))
     ref = yolo_ref.postprocess(raw, (eng.in_h, eng.in_w), (1080, 1920), max_det=eng.max_det,
-                               classes_keep=[2, 7] if case == "classes" else ())
+                               max_nms=max_nms, classes_keep=[2, 7] if case == "classes" else ())
     np.testing.assert_array_equal(dets[0, :int(n_[0])].cpu().numpy(), ref[0])
+    if case == "maxnms":
+        assert int(n_[0]) > 0
+
+
+@pytest.mark.parametrize("n", [20000, 33500])
+def test_nms_config5_candidates(cuda, n):
+    """Config 5 geometry (1280 x 1280, A = 33600 anchors): more candidates
+    than 16384, and (n = 33500) more than max_nms = 30000.  Every candidate
+    is sorted; only the top 30000 by score enter the greedy pass (Ultralytics
+    max_nms).  Boxes sit in tight same-class clusters (NMS keeps about one per
+    cluster and class); the 3500 lowest-score boxes form clusters of their own,
+    so they reach the output exactly when they survive the max_nms cut."""
+    rng = np.random.default_rng(n)
+    eng, _ = _engine(1280, 1280, 1, cuda, imgsz=1280, max_det=1024)
+    A = eng.A
+    assert A == 33600
+    n_low = 3500
+
+    def clusters(m, nclu, lo, hi):
+        ctr = rng.uniform(lo, hi, (nclu, 2))
+        k = rng.integers(0, nclu, m)
+        xy = ctr[k] + rng.normal(0, 1.0, (m, 2))
+        return np.concatenate([xy, xy + 60.0 + rng.normal(0, 1.0, (m, 2))], 1), k % 4
+
+    b_lo, c_lo = clusters(n_low, 20, 1000, 1180)
+    b_hi, c_hi = clusters(n - n_low, 64, 0, 900)
+    boxes = np.concatenate([b_lo, b_hi])
+    cls = np.concatenate([c_lo, c_hi])
+    scores = np.concatenate([np.sort(rng.uniform(0.26, 0.4, n_low)),
+                             rng.uniform(0.5, 1.0, n - n_low)])
+    raw = _raw_from_boxes(boxes, scores, cls, A)
+    dets, n_ = eng.nms_from_raw(torch.from_numpy(raw).to(cuda))
+    ref = yolo_ref.postprocess(raw, (eng.in_h, eng.in_w), (1280, 1280), max_det=1024)
+    got = dets[0, :int(n_[0])].cpu().numpy()
+    np.testing.assert_array_equal(got, ref[0])
+    assert int(eng.cand_n[0]) == n
+    low_kept = int((got[:, 4] < 0.45).sum())
+    print(f"n={n}: kept {len(got)}, low-score kept {low_kept}")
+    assert len(got) < 1024
+    assert (low_kept == 0) if n > 30000 else (low_kept > 0)
 
 
 def _iou(a, b):

@@ -28,9 +28,7 @@ def test_clahe_bit_exact(cuda, H, W, tiles, clip):
 @pytest.mark.parametrize("k", [3, 5, 7, 9])
 def test_median_bit_exact(cuda, H, W, k):
     from rvs_amd import kernels
-    if H * W > 700_000 and k > 3:
-        pytest.skip("oracle counting median too slow at this size; k=3 covers 1080p")
-    img = road_frame(H, W, seed=k * 31 + H)
+    img = road_frame(H, W, seed=k * 31 + H)  # 1080p k=9: ~2.5 s on the OpenMP oracle
     got = kernels.median(_dev(img, cuda), k).cpu().numpy()
     np.testing.assert_array_equal(got, cpu.median(img, k))
 
@@ -46,8 +44,7 @@ def test_fused_clahe_median_equals_chain(cuda, H, W, k):
     fused = kernels.clahe_median(x, 8, 2.0, k).cpu().numpy()
     chain = kernels.median(kernels.clahe_ycrcb(x, 8, 2.0), k).cpu().numpy()
     np.testing.assert_array_equal(fused, chain)
-    if H * W <= 700_000 or k == 3:
-        np.testing.assert_array_equal(fused, cpu.median(cpu.clahe_ycrcb(img, 8, 2.0), k))
+    np.testing.assert_array_equal(fused, cpu.median(cpu.clahe_ycrcb(img, 8, 2.0), k))
 
 
 def test_batched_frames_and_pitch(cuda):

@@ -2,8 +2,12 @@
 world_size 2: each rank owns a disjoint block of camera streams, generates
 exactly the frames a single process would for those streams, runs the
 per-stream chain (oracle preprocess + SORT) with no data exchange, and the
-timed region is reduced with a max over ranks.  The GPU bench uses the same
-functions (bench.py -> rvs_amd.shard) with the nccl (RCCL) backend."""
+timed region is reduced with a max over ranks.  The ranks run bench.py's
+own rank logic -- rvs_amd.shard.init_from_env + bench.rank_job (warm-up,
+prepare, shard.timed_job: barrier, sync, run, sync, barrier, MAX over
+ranks, whole-job rate) -- with a CPU stub job in place of the GPU engine
+and real perf_counter timing, so the code torchrun runs on the GPUs (with
+the nccl = RCCL backend) is the code under test here."""
 import os
 import socket
 
@@ -19,36 +23,62 @@ def _free_port():
         return s.getsockname()[1]
 
 
+class _CpuJob:
+    """bench.BenchJob's interface (warmup / prepare / run / sync / units)
+    over the oracle chain of this rank's streams."""
+
+    def __init__(self, S, F, rank):
+        from rvs_amd.shard import rank_streams
+        from rvs_amd.synth import road_frames
+        self.ids = rank_streams(S, rank)
+        self.fr = road_frames(S, F, 48, 64, device="cpu", stream_offset=self.ids.start).numpy()
+        self.S, self.F = S, F
+        self.units = S * F
+        self.out = {}
+        self.calls = []
+
+    def warmup(self):
+        self.calls.append("warmup")
+
+    def prepare(self):
+        self.calls.append("prepare")
+
+    def run(self):
+        from oracle import cpu, sort_ref
+        from rvs_amd.config import load_config
+        self.calls.append("run")
+        cfg = load_config()["tracking"]
+        for j, sid in enumerate(self.ids):
+            trk = sort_ref.SortTracker(cfg)
+            rng = np.random.default_rng(sid)
+            base = rng.uniform(0, 40, (3, 2))
+            tracks = []
+            for f in range(self.F):
+                proc = cpu.median(cpu.clahe_ycrcb(self.fr[f, j]), 3)
+                dets = [sort_ref.Det(x + 2 * f, y, x + 2 * f + 8, y + 8, 0.9, 2) for x, y in base]
+                trk.update(dets, f / 30.0)
+                tracks.append(([d.track_id for d in dets], int(proc.sum())))
+            self.out[sid] = tracks
+
+    def sync(self):
+        self.calls.append("sync")
+
+
 def _worker(rank, world, port, S, F, q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [os.path.dirname(here), os.path.join(os.path.dirname(here),
                                                           "road-vision-system_amd"), here]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank), OMP_NUM_THREADS="2")
     import torch.distributed as dist
-    from oracle import cpu, sort_ref
-    from rvs_amd.config import load_config
-    from rvs_amd.shard import job_throughput, max_over_ranks, rank_streams
-    from rvs_amd.synth import road_frames
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    ids = rank_streams(S, rank)
-    fr = road_frames(S, F, 48, 64, device="cpu", stream_offset=ids.start).numpy()
-    cfg = load_config()["tracking"]
-    out = {}
-    for j, sid in enumerate(ids):
-        trk = sort_ref.SortTracker(cfg)
-        rng = np.random.default_rng(sid)
-        base = rng.uniform(0, 40, (3, 2))
-        tracks = []
-        for f in range(F):
-            proc = cpu.median(cpu.clahe_ycrcb(fr[f, j]), 3)
-            dets = [sort_ref.Det(x + 2 * f, y, x + 2 * f + 8, y + 8, 0.9, 2) for x, y in base]
-            trk.update(dets, f / 30.0)
-            tracks.append(([d.track_id for d in dets], int(proc.sum())))
-        out[sid] = tracks
-    elapsed = 0.1 * (rank + 1)
-    mx = max_over_ranks(elapsed)
-    q.put((rank, list(ids), out, mx, job_throughput(S * F, world, mx)))
+    import bench
+    from rvs_amd.shard import init_from_env
+    r, w, _ = init_from_env("gloo")
+    assert (r, w) == (rank, world) and dist.is_initialized()
+    job = _CpuJob(S, F, rank)
+    t = bench.rank_job(job, "cpu")
+    q.put((rank, list(job.ids), job.out, t, job.calls))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -66,12 +96,17 @@ def test_two_rank_sharding_matches_single_process():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    res.sort()
+    res.sort(key=lambda r: r[0])
     # disjoint, covering stream blocks, as partition() lays them out
     assert [r[1] for r in res] == [list(x) for x in partition(S * world, world)]
-    # max over ranks and whole-job throughput
-    assert all(abs(r[3] - 0.2) < 1e-12 for r in res)
-    assert all(abs(r[4] - S * F * world / 0.2) < 1e-6 for r in res)
+    # bench.rank_job's order of operations on every rank
+    assert all(r[4] == ["warmup", "prepare", "sync", "run", "sync"] for r in res)
+    # the reported time is the MAX of the ranks' measured times, and the
+    # whole-job rate is every rank's frames over it
+    mx = max(r[3]["local_s"] for r in res)
+    assert all(r[3]["local_s"] > 0 for r in res)
+    assert all(r[3]["elapsed_s"] == mx for r in res)
+    assert all(abs(r[3]["value"] - S * F * world / mx) < 1e-9 * r[3]["value"] for r in res)
     # each rank's per-stream results equal a single process running all streams
     import sys
     from oracle import cpu, sort_ref
