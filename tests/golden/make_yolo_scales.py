@@ -5,8 +5,22 @@ reference's .MISSING_LARGE_BLOBS and there is no network).  A trained,
 BN-fused YOLOv8 keeps every conv's pre-activation at O(1) scale; random
 He-normal weights do not (activations vanish or explode through 60+ convs).
 This script normalises every conv per output channel like a fused BN
-(layer-sequential: mean 0 / std 1 pre-activation on synthetic road frames,
-using the fp32 CPU oracle forward), then sets the head (DFL logits std 2.5,
+(layer-sequential: std 1 pre-activation on synthetic road frames, using the
+fp32 CPU oracle forward), with a per-channel pre-activation MEAN drawn from
+U(1, 2) for the SiLU convs.  A zero mean puts the random network in the
+chaotic regime (round 1: input noise of 1e-4 moved candidate boxes by 3 px
+at p99, so bf16 rounding flips decided whole detections); a positive mean
+keeps the SiLUs nearer their linear branch, the ordered regime a trained
+network sits in (larger means waste bf16 precision on the mean instead).
+It then sets the head: DFL logits std 0.7 (a box's four sides are then not
+decided by a near-tie of two bins), class logits std 1.0 with a mean that
+makes 1.2 % of the anchors candidates and a +3 prior on the road classes
+0,2,3,5,7.  tools/calib_search.py measures the choice (1080p road frames):
+input noise 1e-4 -> candidate boxes 0.5 px at p99; a 1e-7 relative change
+of every conv output before its bf16 rounding (what a different f32
+accumulation order does) -> 96 % of the quantised oracle's detections
+unchanged (class, IoU >= 0.9) -- the floor for the GPU-vs-oracle test;
+about 40 detections per frame after the class filter. (DFL logits std 2.5,
 class logits std 1.0 with a mean that yields a few hundred NMS candidates per
 1080p frame and a +1 prior on the road classes 0,2,3,5,7), and writes the
 per-channel weight scale and bias (scale, shift: w' = w*scale,
@@ -33,10 +47,11 @@ from oracle import cpu, yolo_ref  # noqa: E402
 OUT = os.path.join(REPO, "road-vision-system_amd", "rvs_amd", "detect", "data",
                    "synthetic_calib.npz")
 ROAD = (0, 2, 3, 5, 7)
+MU = (1.0, 2.0)  # pre-activation mean range of the SiLU convs (ordered regime)
 
 
 def calibrate(variant, seed=0, H=1080, W=1920, box_std=2.5, cls_std=1.0, target_cand=0.04,
-              nframes=2):
+              nframes=2, mu=(0.0, 0.0), road_prior=1.0):
     specs, _ = yolo_ref.conv_specs(variant)
     rng = np.random.default_rng(seed)
     frames = [road_frame(H, W, seed=100 + s) for s in range(nframes)]
@@ -54,14 +69,15 @@ def calibrate(variant, seed=0, H=1080, W=1920, box_std=2.5, cls_std=1.0, target_
     for n, ci, co, k, s, act in specs:
         stat = {}
 
-        def conv(self, name, t, _n=n):
+        def conv(self, name, t, res=None, _n=n):
             w, b, st, kk, a = self.p[name]
             y = F.conv2d(t, w, b, stride=st, padding=kk // 2)
             if name == _n:
                 stat["mean"] = y.mean((0, 2, 3)).numpy()
                 stat["std"] = y.std((0, 2, 3)).numpy()
                 raise StopIteration
-            return F.silu(y) if a else y
+            y = F.silu(y) if a else y
+            return y if res is None else res + y
 
         yolo_ref.YoloRef.conv = conv
         try:
@@ -70,16 +86,18 @@ def calibrate(variant, seed=0, H=1080, W=1920, box_std=2.5, cls_std=1.0, target_
         except StopIteration:
             pass
         yolo_ref.YoloRef.conv = orig
-        t, mu = 1.0, 0.0
+        t, mu_c = 1.0, 0.0
+        if act:  # per-channel pre-activation mean of the SiLU convs
+            mu_c = np.random.default_rng([seed, len(out)]).uniform(mu[0], mu[1], co)
         if n.startswith("model.22.cv2.") and n.endswith(".2"):
             t = box_std
         is_cls = n.startswith("model.22.cv3.") and n.endswith(".2")
         if is_cls:
             t = cls_std
         sc = (t / np.maximum(stat["std"], 1e-6)).astype(np.float32)
-        shift = (-stat["mean"] * sc + mu).astype(np.float32)
+        shift = (-stat["mean"] * sc + mu_c).astype(np.float32)
         if is_cls:
-            shift[list(ROAD)] += 1.0
+            shift[list(ROAD)] += road_prior
         w, b, st, kk, a = m.p[n]
         m.p[n] = (w * torch.from_numpy(sc).view(-1, 1, 1, 1), b * torch.from_numpy(sc) +
                   torch.from_numpy(shift), st, kk, a)
@@ -101,7 +119,8 @@ def calibrate(variant, seed=0, H=1080, W=1920, box_std=2.5, cls_std=1.0, target_
 if __name__ == "__main__":
     arrays = {}
     for v, hw in ((0, (1080, 1920)), (2, (540, 960))):
-        cal = calibrate(v, H=hw[0], W=hw[1])
+        cal = calibrate(v, H=hw[0], W=hw[1], mu=MU, box_std=0.7, target_cand=0.012,
+                        road_prior=3.0)
         for n, (sc, sh) in cal.items():
             arrays[f"{v}/{n}/scale"] = sc
             arrays[f"{v}/{n}/shift"] = sh

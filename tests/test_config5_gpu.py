@@ -9,11 +9,11 @@ DESIGN.md).  Checks:
   * one frame against the torch-CPU restatement at the HIP path's storage
     precision (oracle/yolo_ref.py quant=True).  Every YOLOv8m conv is within
     1 bf16 ulp of a float64 recomputation (test_yolo_layers_gpu.py, variant
-    2), so the remaining whole-network gap is bf16 rounding amplified through
-    83 convs of synthetic weights (v8n has 63; test_detect_gpu.py explains the
-    amplification).  Measured on MI355X: class-score |d| 0.080 at p99.9,
-    box xywh within 1 px + 1 % for 93.8 % of anchors.  Asserted:
-    p99.9 <= 0.15 and >= 90 %;
+    2), so the remaining whole-network gap is bf16 rounding flips carried
+    through 83 convs of synthetic weights (test_detect_gpu.py).  Measured on
+    MI355X (r02, ordered-regime weights): class-score |d| 0.0058 at p99.9,
+    box xywh within 1 px + 1 % for 99.97 % of anchors.  Asserted:
+    p99.9 <= 0.02 and >= 99.5 %;
   * NMS on the GPU's raw prediction is bit-exact against the restated NMS.
 Layer-by-layer YOLOv8m parity is in test_yolo_layers_gpu.py (variant 2).
 """
@@ -57,8 +57,10 @@ def test_v8m_1280_fog_batch16(cuda):
     frac_box = float((db <= 1.0 + 0.01 * np.abs(ref[:, :4])).mean())
     print(f"v8m 1280: score |d| p99.9 {np.percentile(ds, 99.9):.4f} max {ds.max():.4f}; "
           f"box within tol {frac_box:.5f}")
-    assert np.percentile(ds, 99.9) <= 0.15
-    assert frac_box >= 0.90
+    # measured r02 (ordered-regime synthetic weights): score p99.9 0.0058,
+    # 99.97 % of box coordinates within 1 px + 1 %
+    assert np.percentile(ds, 99.9) <= 0.02
+    assert frac_box >= 0.995
 
     dets, n = eng.nms_from_raw(raw)
     dets, n = dets.cpu().numpy(), n.cpu().numpy()

@@ -5,20 +5,21 @@ Tolerances (stated here, see DESIGN.md "Parity"):
     (boxes, scores, classes and order).
   * Every conv kernel is checked layer by layer (test_yolo_layers_gpu.py:
     within 1 bf16 ulp of a float64 recomputation from the GPU's own inputs).
-  * Whole-network comparisons are statistical, because the synthetic
-    (random, LSUV-calibrated) weights amplify perturbations: on the CPU, input
-    noise of 1e-4 moves boxes by 2.8 px at p99 and 34 px at worst, so a
-    single bf16 rounding flip deep in the net can move a few anchors a lot.
+  * Whole-network comparisons are statistical: a bf16 rounding that flips
+    because of a different f32 accumulation order moves later layers.  The
+    synthetic weights are calibrated into the ordered regime
+    (tests/golden/make_yolo_scales.py; round 1's were chaotic: input noise
+    1e-4 moved boxes 2.8 px at p99, now 0.5 px on candidate anchors).
     Measured and asserted here:
       - vs the torch-CPU restatement at the same storage precision
-        (quant=True: bf16 weights/activations, f32 accumulate; differs from
-        the GPU only in accumulation order): class-score |d| <= 0.02 at the
-        99.9th percentile, box xywh |d| <= 1 px + 1 % for >= 95 % of anchors;
+        (quant=True: bf16 weights/activations, f32 accumulate): class-score
+        |d| <= 0.005 at the 99.9th percentile, box xywh |d| <= 1 px + 1 % for
+        >= 99.9 % of anchors;
       - vs the pure fp32 restatement (the reference's precision):
-        class-score |d| <= 0.05 at p99.9, box |d| <= 4 px + 3 % for >= 97 %;
-      - end to end (letterbox -> forward -> NMS): >= 50 % of the fp32
-        oracle's detections with score >= 0.35 are matched by a GPU detection
-        of the same class with IoU >= 0.9.
+        class-score |d| <= 0.01 at p99.9, box |d| <= 2 px + 2 % for >= 99.9 %;
+      - end to end (letterbox -> forward -> NMS -> class filter): >= 95 % of
+        the quantised oracle's detections matched by a GPU detection of the
+        same class with IoU >= 0.9 and vice versa (>= 85 % vs fp32).
     Ultralytics itself is absent, so detector parity against real
     Ultralytics (and real weights) is unpinned.
 """
@@ -58,10 +59,10 @@ def test_forward_matches_oracle(cuda, H, W, B, quant):
     assert got.shape == ref.shape
     ds = np.abs(got[:, 4:] - ref[:, 4:])
     db = np.abs(got[:, :4] - ref[:, :4])
-    if quant:
-        s_tol, b_abs, b_rel, b_frac = 0.02, 1.0, 0.01, 0.95
-    else:
-        s_tol, b_abs, b_rel, b_frac = 0.05, 4.0, 0.03, 0.97
+    if quant:  # measured r02: score p99.9 0.0033, 99.99 % of boxes within 1 px + 1 %
+        s_tol, b_abs, b_rel, b_frac = 0.005, 1.0, 0.01, 0.999
+    else:  # measured r02: score p99.9 0.0061, box p99 2.4 px
+        s_tol, b_abs, b_rel, b_frac = 0.01, 2.0, 0.02, 0.999
     frac_box = float((db <= b_abs + b_rel * np.abs(ref[:, :4])).mean())
     print(f"quant={quant} score |d| max {ds.max():.4f} p99.9 {np.percentile(ds, 99.9):.4f}; "
           f"box |d| max {db.max():.2f} px p99 {np.percentile(db, 99):.3f}, "
@@ -176,27 +177,53 @@ def _iou(a, b):
     return inter / u if u > 0 else 0
 
 
+def _match_frac(a, b, min_score=0.27):
+    """Fraction of the rows of `a` with score >= min_score matched by a row of
+    `b` with the same class and IoU >= 0.9 (per image lists of (n, 6) rows).
+    Rows within 0.02 of conf = 0.25 are left out: any change of the last
+    bits decides whether such a candidate exists at all."""
+    tot = hit = 0
+    for x, y in zip(a, b):
+        for r in x:
+            if r[4] < min_score:
+                continue
+            tot += 1
+            hit += any(int(g[5]) == int(r[5]) and _iou(g, r) >= 0.9 for g in y)
+    return hit, tot
+
+
 @pytest.mark.parametrize("H,W", [(1080, 1920), (640, 640)])
 def test_end_to_end_detections(cuda, H, W):
-    B = 2
-    eng, flat = _engine(H, W, B, cuda)
+    """letterbox -> forward -> NMS -> class filter on the GPU vs the oracle's
+    detections (the reference's default classes_keep [0, 2, 3, 5, 7]).
+    Against YoloRef(quant=True) -- the same storage precision (bf16 weights
+    and activations, f32 accumulation), so the two differ only in
+    accumulation order and the hardware exp / reciprocal: >= 95 % of the
+    detections match (same class, IoU >= 0.9) in both directions.  The
+    oracle's own floor under a 1e-7 relative change of every conv output
+    before its bf16 rounding is ~96-98 % (tools/calib_search.py; NMS picks
+    between near-tied overlapping candidates).  Against the fp32 restatement
+    (the reference's precision): >= 85 % (bf16 storage itself, measured
+    offline at ~90 %)."""
+    B = 4
+    keep = [0, 2, 3, 5, 7]
+    eng, flat = _engine(H, W, B, cuda, classes_keep=keep)
     fr = _frames(H, W, B, seed=20)
     dets, n = eng.run(torch.from_numpy(fr).to(cuda))
     dets, n = dets.cpu().numpy(), n.cpu().numpy()
-    lb = eng.letterbox(torch.from_numpy(fr).to(cuda)).cpu().numpy()
-    raw = yolo_ref.YoloRef(0, flat).forward(yolo_ref.preprocess(lb)).numpy()
-    ref = yolo_ref.postprocess(raw, (eng.in_h, eng.in_w), (H, W))
-    matched = total = 0
-    for b in range(B):
-        g = dets[b, :n[b]]
-        for r in ref[b]:
-            if r[4] < 0.35:
-                continue
-            total += 1
-            if any(int(x[5]) == int(r[5]) and _iou(x, r) >= 0.9 for x in g):
-                matched += 1
-    print(f"matched {matched}/{total}")
-    assert total > 0 and matched >= 0.5 * total
+    got = [dets[b, :n[b]] for b in range(B)]
+    lb = yolo_ref.preprocess(eng.letterbox(torch.from_numpy(fr).to(cuda)).cpu().numpy())
+    out = {}
+    for quant in (True, False):
+        raw = yolo_ref.YoloRef(0, flat, quant=quant).forward(lb).numpy()
+        ref = yolo_ref.postprocess(raw, (eng.in_h, eng.in_w), (H, W), classes_keep=keep)
+        out[quant] = (_match_frac(ref, got), _match_frac(got, ref))
+        print(f"quant={quant}: oracle dets matched by GPU {out[quant][0]}, "
+              f"GPU dets matched by oracle {out[quant][1]}; all rows: {_match_frac(ref, got, 0)}")
+    (h1, t1), (h2, t2) = out[True]
+    assert t1 > 0 and h1 >= 0.95 * t1 and h2 >= 0.95 * t2
+    (h1, t1), (h2, t2) = out[False]
+    assert h1 >= 0.85 * t1 and h2 >= 0.85 * t2
 
 
 def test_detector_api_returns_detections(cuda):

@@ -1,0 +1,17 @@
+# rocprofv3 kernel trace of bench.py's timed region (tools/trace_window.py
+# keeps the dispatches between the rv_trace_marker kernels), with the conv
+# configs saved by a preceding `bench.py --tune-save $TUNE` so no autotuner
+# launch is in the trace.  usage: TAG=r02 TUNE=gpurun_out/tune.json bash tools/gpu_profile.sh
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/${TAG:-prof}
+STEPS=${STEPS:-60}
+mkdir -p "$OUT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/raw" -o trace -- \
+  python3 bench.py --tune-load "$TUNE" --warmup 1 --steps "$STEPS" --no-cpu-baseline \
+  --conv-timing none ${BENCH_ARGS:-} > "$OUT/bench_profiled.json" 2> "$OUT/bench_profiled.err" || exit $?
+KT=$(find "$OUT/raw" -name "*kernel_trace.csv" | head -1)
+ST=$(find "$OUT/raw" -name "*kernel_stats.csv" | head -1)
+cp "$ST" "$OUT/rocprof_kernel_stats_whole_run.csv"
+python3 tools/trace_window.py "$KT" "$STEPS" "$OUT/timed" || exit $?
+rm -rf "$OUT/raw"
