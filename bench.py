@@ -78,6 +78,9 @@ def parse_args(argv=None):
                     help="pipelined steps: 3 = Y(k) || P(k+1) || T(k-1), 2 = [T(k-1) || P(k)] -> Y(k)")
     ap.add_argument("--graph-chunk", type=int, default=None,
                     help="pipeline steps per captured graph (default 8, RV_GRAPH_CHUNK; 0 = all)")
+    ap.add_argument("--lanes", type=int, default=int(os.environ.get("RV_LANES", 1)),
+                    help="forward lanes: the YOLO forwards of this many consecutive steps run "
+                         "concurrently (engine.OverlappedSteps dependency-graph schedule)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one graph per step; no overlap of step k's NMS+SORT with step k+1")
     return ap.parse_args(argv)
@@ -93,7 +96,8 @@ class BenchJob:
         self.args, self.dev = args, dev
         self.cfg = bench_config()
         self.S, self.K, self.Wm = args.streams, args.steps, args.warmup
-        self.eng = RoadVisionEngine(self.cfg, self.S, (H, W), device=dev, tmax=args.tmax)
+        self.eng = RoadVisionEngine(self.cfg, self.S, (H, W), device=dev, tmax=args.tmax,
+                                    lanes=args.lanes)
         self.frames = road_frames(self.S, self.Wm + self.K, H, W, device=dev,
                                   stream_offset=rank_streams(self.S, rank).start)
         self.ts = torch.tensor([[f / 30.0] * self.S for f in range(self.Wm + self.K)],
@@ -372,9 +376,13 @@ def main(argv=None):
                                      (not args.no_autotune)),
                    "execution": "eager" if args.eager else
                                 ("graph per step" if args.no_pipeline else
-                                 f"graphs, {args.depth}-stage software pipeline over steps "
-                                 "(preprocess / YOLO / NMS+SORT+hand-back of consecutive steps "
-                                 f"overlap), {chunk_desc} steps per graph")},
+                                 (f"graphs, dependency-graph pipeline with {args.lanes} concurrent "
+                                  "YOLO forwards (preprocess runs ahead, NMS+SORT+hand-back "
+                                  f"follows in step order), {chunk_desc} steps per graph"
+                                  if args.lanes > 1 else
+                                  f"graphs, {args.depth}-stage software pipeline over steps "
+                                  "(preprocess / YOLO / NMS+SORT+hand-back of consecutive steps "
+                                  f"overlap), {chunk_desc} steps per graph"))},
         "roofline": roof,
         "end_to_end_roofline_frac": round(value / world * (BYTES_PER_FRAME / (PEAK_HBM * 1e9) +
                                                            FLOP_PER_FRAME / (PEAK_BF16 * 1e12)), 5),

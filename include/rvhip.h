@@ -245,22 +245,29 @@ int rv_candidates_from_raw(const float* raw, int B, int nc, int A, float conf, v
 /* ------------------------------------------------------------------------ */
 size_t rv_sort_state_bytes(int S, int tmax);
 size_t rv_sort_ws_bytes(int S, int tmax, int dmax);
-/* Zero the state (no tracks, next_id = 1); synchronises `stream`. */
+/* Zero the state (no tracks, next_id = 1); synchronises `stream`.  Layout:
+ * per-stream headers, list orders (tmax int32 each) and track pools (tmax
+ * slots each); a track keeps its slot for life, the reference's list order
+ * is the order array. */
 int rv_sort_init(void* state, int S, int tmax, void* stream);
-/* One frame per stream.  state_in is consumed (used as the work copy);
- * state_out receives the new state (ping-pong).  dets: S x dmax x 6
- * {x1,y1,x2,y2,conf,cls} f32 (post class-filter), dcount[S]; ts[S] seconds.
- * params6 = {max_staleness, min_hits, iou_threshold, speed_window,
- * max_distance (<0 = None), 0}.  H9 (nullable = no projector): row-major
- * f64 homography; origin2: projector origin (f32).  Outputs per detection
- * (S x dmax): track id (-1 = None), distance_m and speed_kmh (NaN = None). */
+/* One frame per stream, three stream-ordered launches (KF predict over every
+ * track; one workgroup per stream for _associate + bookkeeping; KF update /
+ * new tracks over every detection).  The update runs in place on state_out;
+ * pass state_in == state_out (if they differ, state_in is first copied to
+ * state_out).  dets: S x dmax x 6 {x1,y1,x2,y2,conf,cls} f32 (post
+ * class-filter), dcount[S]; ts[S] seconds.  params6 = {max_staleness,
+ * min_hits, iou_threshold, speed_window, max_distance (<0 = None), 0}.  H9
+ * (nullable = no projector): row-major f64 homography; origin2: projector
+ * origin (f32).  Outputs per detection (S x dmax): track id (-1 = None),
+ * distance_m and speed_kmh (NaN = None).  tmax <= 8192 and the association
+ * workgroup's LDS (about 41 B x tmax + 28 B x dmax + 32 KB) <= 160 KB. */
 int rv_sort_update(void* state_in, void* state_out, int S, int tmax, const float* dets,
                    const int* dcount, int dmax, const double* ts, const double* params6,
                    const double* H9, const float* origin2, void* ws, size_t ws_bytes,
                    int* out_id, double* out_dist, double* out_speed, void* stream);
 /* Per-stream capacity report (device outputs, S ints each): live tracks T,
  * next track id, and the sticky overflow flag -- 1 once a frame had more
- * live + new tracks than tmax; the new tracks that did not fit were dropped
+ * surviving + new tracks than tmax; the new tracks that did not fit were dropped
  * (their ids were still handed out), so that stream's ids diverge from the
  * reference's unbounded track list from then on.  next_id_out / overflow_out
  * are nullable. */

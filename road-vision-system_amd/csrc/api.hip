@@ -13,7 +13,7 @@ void set_error(const char* fmt, ...) {
 }
 }  // namespace rv
 
-extern "C" int rv_abi_version(void) { return 3; }
+extern "C" int rv_abi_version(void) { return 4; }
 extern "C" const char* rv_last_error(void) { return rv::g_err; }
 
 // Trace marker: an empty one-wave kernel whose dispatch brackets a region of

@@ -28,7 +28,7 @@
 namespace rv {
 
 constexpr int kHist = 33;     // speed history (32 kept after each append)
-constexpr int kKeyCap = 4096;
+constexpr int kKeyCap = 1024;  // sorted IoU pairs in LDS (8 KB); more -> the argmax loop over M
 
 struct Track {
   double x[7];
@@ -249,69 +249,134 @@ __device__ void track_init(Track& t, int id, const float* det, double ts) {
 }
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void sort_update_kernel(
-    const StreamHdr* __restrict__ hin, Track* __restrict__ tin, StreamHdr* __restrict__ hout,
-    Track* __restrict__ tout, const float* __restrict__ dets, const int* __restrict__ dcount,
-    const double* __restrict__ ts_arr, SortParams p, float* __restrict__ iou_ws,
-    int* __restrict__ out_id, double* __restrict__ out_dist, double* __restrict__ out_speed) {
+// One frame of every stream in three launches (rv_sort_update):
+//
+//   sort_predict_kernel    one thread per live track of every stream: KF
+//                          predict (sort_tracker.py:228-229), the predicted
+//                          box and last_update_ts to the workspace;
+//   sort_associate_kernel  one workgroup per stream: _iou_matrix pairs >= thr,
+//                          sorted (IoU desc, flat index asc), the greedy walk
+//                          resolved 64 pairs at a time by wave ballots; the
+//                          bookkeeping of :234-276 -- unmatched tracks'
+//                          hit_streak = 0, new-track ranks / ids in det
+//                          order, pruning by staleness, the new list order
+//                          and a pool slot for every new track -- all by
+//                          block prefix scans;
+//   sort_update_kernel     one thread per detection of every stream: KF
+//                          update + metrics of its matched track, or the
+//                          new track's init + metrics; the per-detection
+//                          outputs.
+//
+// Tracks live in a fixed per-stream pool of tmax slots; the reference's
+// list order is an index array (order[i] = slot of the i-th track), so a
+// frame never copies a track.  Survivors keep their order, new tracks are
+// appended in detection order and take free slots (pruned tracks' slots are
+// reused in the same frame).  Capacity: survivors + new tracks > tmax drops
+// the new tracks that do not fit (their ids are still handed out) and sets
+// the stream's sticky overflow flag (rv_sort_stats).
+// ---------------------------------------------------------------------------
+constexpr int kAssocThreads = 1024;
+
+struct SortWs {  // per-frame workspace views (rv_sort_ws_bytes)
+  float* M;         // S x tmax x dmax IoU matrix (argmax fallback only)
+  float4* tbox;     // S x tmax predicted boxes (list order)
+  double* tupd;     // S x tmax last_update_ts (list order)
+  int2* det_job;    // S x dmax: {slot, id} per detection (see sort_update_kernel)
+};
+
+__global__ __launch_bounds__(256) void sort_predict_kernel(const StreamHdr* __restrict__ hdr,
+                                                           const int* __restrict__ order,
+                                                           Track* __restrict__ pool,
+                                                           const double* __restrict__ ts_arr,
+                                                           int tmax, SortWs ws) {
+  const int s = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= hdr[s].T) return;
+  const double ts = ts_arr[s];
+  Track& tr = pool[(size_t)s * tmax + order[(size_t)s * tmax + i]];
+  kf_predict(tr, ts - tr.t_pred);
+  tr.t_pred = ts;
+  ws.tbox[(size_t)s * tmax + i] = x_to_bbox(tr.x);
+  ws.tupd[(size_t)s * tmax + i] = tr.t_upd;
+}
+
+// Exclusive prefix of flag(i) over [0, n) for a kAssocThreads block,
+// chunked: out[i] = rank of i among the flagged, -1 if not flagged; returns
+// the total.  `wtot`: kAssocThreads / 64 ints of LDS scratch.
+template <class F>
+__device__ int block_rank(F flag, int n, int* out, int* wtot) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int base = 0;
+  for (int c0 = 0; c0 < n; c0 += kAssocThreads) {
+    const int i = c0 + tid;
+    const bool f = i < n && flag(i);
+    const unsigned long long m = __ballot(f);
+    if (lane == 0) wtot[w] = __popcll(m);
+    __syncthreads();
+    int pre = base, tot = 0;
+    for (int k = 0; k < kAssocThreads / 64; ++k) {
+      pre += k < w ? wtot[k] : 0;
+      tot += wtot[k];
+    }
+    if (i < n) out[i] = f ? pre + __popcll(m & ((1ull << lane) - 1ull)) : -1;
+    base += tot;
+    __syncthreads();
+  }
+  return base;
+}
+
+__global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
+    StreamHdr* __restrict__ hdr, int* __restrict__ order, Track* __restrict__ pool,
+    const float* __restrict__ dets, const int* __restrict__ dcount,
+    const double* __restrict__ ts_arr, SortParams p, SortWs ws) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  float4* tbox = (float4*)smem;                       // tmax
-  float4* dbox = tbox + p.tmax;                       // dmax
-  uint64_t* keys = (uint64_t*)(dbox + p.dmax);        // kKeyCap
-  int* det_match = (int*)(keys + kKeyCap);            // dmax: matched track or -1
-  int* trk_match = det_match + p.dmax;                // tmax: matched det or -1
-  int* keep_pos = trk_match + p.tmax;                 // tmax + dmax: output slot or -1
-  __shared__ int s_cnt, s_red_v[4], s_red_i[4];
+  float4* tbox = (float4*)smem;                     // tmax
+  float4* dbox = tbox + p.tmax;                     // dmax
+  uint64_t* keys = (uint64_t*)(dbox + p.dmax);      // kKeyCap
+  double* tupd = (double*)(keys + kKeyCap);         // tmax
+  int* det_match = (int*)(tupd + p.tmax);           // dmax: matched track (list index) or -1
+  int* trk_match = det_match + p.dmax;              // tmax: matched det or -1
+  int* ord = trk_match + p.tmax;                    // tmax: the old list order (slots)
+  int* rank_t = ord + p.tmax;                       // tmax: survivor rank
+  int* frank = rank_t + p.tmax;                     // tmax: free-slot rank
+  int* rank_d = frank + p.tmax;                     // dmax: new-track rank
+  int* newslot = rank_d + p.dmax;                   // dmax: slot of the r-th new track
+  uint8_t* used = (uint8_t*)(newslot + p.dmax);     // tmax
+  __shared__ int s_cnt, s_red_v[16], s_red_i[16], wtot[16];
 
   const int s = blockIdx.x;
-  const int tid = threadIdx.x;
-  const StreamHdr h = hin[s];
-  Track* Wk = tin + (size_t)s * p.tmax;  // work copy (the consumed input state)
-  Track* T_out = tout + (size_t)s * p.tmax;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const StreamHdr h = hdr[s];
   const int T = h.T;
   int D = dcount[s];
-  if (D > p.dmax) D = p.dmax;
+  D = D < 0 ? 0 : (D > p.dmax ? p.dmax : D);
   const float* dd = dets + (size_t)s * p.dmax * 6;
   const double ts = ts_arr[s];
-  int* oid = out_id + (size_t)s * p.dmax;
-  double* odist = out_dist + (size_t)s * p.dmax;
-  double* ospd = out_speed + (size_t)s * p.dmax;
+  int2* job = ws.det_job + (size_t)s * p.dmax;
+  int* ord_g = order + (size_t)s * p.tmax;
+  Track* pl = pool + (size_t)s * p.tmax;
 
-  for (int d = tid; d < p.dmax; d += 256) {
-    oid[d] = -1;
-    odist[d] = NAN;
-    ospd[d] = NAN;
-  }
-  if (T == 0 && D == 0) {
-    if (tid == 0) hout[s] = h;
-    return;
-  }
-  // predict every track in place in the work copy
-  for (int t = tid; t < T; t += 256) {
-    Track& tr = Wk[t];
-    kf_predict(tr, ts - tr.t_pred);
-    tr.t_pred = ts;
-    tbox[t] = x_to_bbox(tr.x);
+  for (int t = tid; t < T; t += kAssocThreads) {
+    tbox[t] = ws.tbox[(size_t)s * p.tmax + t];
+    tupd[t] = ws.tupd[(size_t)s * p.tmax + t];
+    ord[t] = ord_g[t];
     trk_match[t] = -1;
   }
-  for (int d = tid; d < D; d += 256) {
+  for (int d = tid; d < D; d += kAssocThreads) {
     dbox[d] = make_float4(dd[d * 6], dd[d * 6 + 1], dd[d * 6 + 2], dd[d * 6 + 3]);
     det_match[d] = -1;
   }
   if (tid == 0) s_cnt = 0;
   __syncthreads();
 
-  // ---- association
+  // ---- association (_associate, sort_tracker.py:182-210)
   if (T > 0 && D > 0) {
-    float* M = iou_ws + (size_t)s * p.tmax * p.dmax;
-    for (int i = tid; i < T * D; i += 256) {
+    for (int i = tid; i < T * D; i += kAssocThreads) {
       const int t = i / D, d = i - (i / D) * D;
       const float v = iou_f32(tbox[t], dbox[d]);
-      M[i] = v;
       if ((double)v >= p.iou_thr) {
         const int k = atomicAdd(&s_cnt, 1);
-        if (k < kKeyCap)
-          keys[k] = ((uint64_t)(~__float_as_uint(v)) << 32) | (uint64_t)(uint32_t)i;
+        if (k < kKeyCap) keys[k] = ((uint64_t)(~__float_as_uint(v)) << 32) | (uint64_t)(uint32_t)i;
       }
     }
     __syncthreads();
@@ -319,11 +384,11 @@ __global__ __launch_bounds__(256) void sort_update_kernel(
     if (cnt <= kKeyCap) {
       int np2 = 1;
       while (np2 < cnt) np2 <<= 1;
-      for (int i = cnt + tid; i < np2; i += 256) keys[i] = ~0ull;
+      for (int i = cnt + tid; i < np2; i += kAssocThreads) keys[i] = ~0ull;
       __syncthreads();
       for (int size = 2; size <= np2; size <<= 1)
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-          for (int i = tid; i < np2 / 2; i += 256) {
+          for (int i = tid; i < np2 / 2; i += kAssocThreads) {
             const int lo = 2 * i - (i & (stride - 1));
             const int hi = lo + stride;
             const bool up = (lo & size) == 0;
@@ -335,22 +400,48 @@ __global__ __launch_bounds__(256) void sort_update_kernel(
           }
           __syncthreads();
         }
-      if (tid == 0) {
-        for (int k = 0; k < cnt; ++k) {
-          const int i = (int)(keys[k] & 0xFFFFFFFFu);
-          const int t = i / D, d = i - (i / D) * D;
-          if (trk_match[t] < 0 && det_match[d] < 0) {
-            trk_match[t] = d;
-            det_match[d] = t;
+      // greedy walk in (IoU desc, flat index asc) order, 64 pairs at a time:
+      // a pair is accepted iff its row and column are still free; inside a
+      // chunk the lowest remaining lane is accepted and the lanes sharing its
+      // row or column are dropped (wave-uniform ballot loop)
+      if (tid < 64) {
+        for (int base = 0; base < cnt; base += 64) {
+          const int i = base + lane;
+          int t = -1, d = -2;
+          bool ok = false;
+          if (i < cnt) {
+            const int f = (int)(keys[i] & 0xFFFFFFFFu);
+            t = f / D;
+            d = f - t * D;
+            ok = trk_match[t] < 0 && det_match[d] < 0;
           }
+          unsigned long long m = __ballot(ok);
+          while (m) {
+            const int q = __ffsll((long long)m) - 1;
+            const int tq = __shfl(t, q), dq = __shfl(d, q);
+            if (lane == q) {
+              trk_match[t] = d;
+              det_match[d] = t;
+            }
+            m &= ~__ballot(t == tq || d == dq);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          __builtin_amdgcn_wave_barrier();
         }
       }
     } else {
-      // literal reference loop: argmax (first max) -> accept -> mask
+      // more qualifying pairs than keys: the literal reference loop (argmax
+      // with the first maximum, accept, mask row and column) over M in HBM
+      float* M = ws.M + (size_t)s * p.tmax * p.dmax;
+      for (int i = tid; i < T * D; i += kAssocThreads) {
+        const int t = i / D, d = i - (i / D) * D;
+        M[i] = iou_f32(tbox[t], dbox[d]);
+      }
+      __syncthreads();
       for (;;) {
         float bv = -INFINITY;
         int bi = 0x7FFFFFFF;
-        for (int i = tid; i < T * D; i += 256) {
+        for (int i = tid; i < T * D; i += kAssocThreads) {
           const float v = M[i];
           if (v > bv || (v == bv && i < bi)) {
             bv = v;
@@ -365,14 +456,14 @@ __global__ __launch_bounds__(256) void sort_update_kernel(
             bi = oi;
           }
         }
-        if ((tid & 63) == 0) {
+        if (lane == 0) {
           s_red_v[tid >> 6] = __float_as_int(bv);
           s_red_i[tid >> 6] = bi;
         }
         __syncthreads();
         bv = __int_as_float(s_red_v[0]);
         bi = s_red_i[0];
-        for (int w = 1; w < 4; ++w) {
+        for (int w = 1; w < kAssocThreads / 64; ++w) {
           const float ov = __int_as_float(s_red_v[w]);
           if (ov > bv || (ov == bv && s_red_i[w] < bi)) {
             bv = ov;
@@ -386,112 +477,145 @@ __global__ __launch_bounds__(256) void sort_update_kernel(
           trk_match[t] = d;
           det_match[d] = t;
         }
-        for (int j = tid; j < D; j += 256) M[t * D + j] = -1.0f;
-        for (int i = tid; i < T; i += 256) M[i * D + d] = -1.0f;
+        for (int j = tid; j < D; j += kAssocThreads) M[t * D + j] = -1.0f;
+        for (int i = tid; i < T; i += kAssocThreads) M[i * D + d] = -1.0f;
         __syncthreads();
       }
     }
   }
   __syncthreads();
 
-  // ---- update matched tracks, mark missed
-  for (int t = tid; t < T; t += 256) {
-    Track& tr = Wk[t];
-    const int d = trk_match[t];
-    if (d >= 0) {
-      const float* de = dd + d * 6;
-      double z[4];
-      bbox_to_z(de[0], de[1], de[2], de[3], z);
-      kf_update(tr, z);
-      tr.t_pred = ts;
-      tr.t_upd = ts;
-      tr.hits += 1;
-      tr.streak += 1;
-      tr.cls = (int)de[5];
-      tr.conf = de[4];
-      if (p.has_proj) update_metrics(p, tr, de[0], de[1], de[2], de[3], ts);
-      oid[d] = tr.id;
-      if (!isnone(tr.cur_dist)) odist[d] = tr.cur_dist;
-      if (!isnone(tr.cur_speed)) ospd[d] = tr.cur_speed * 3.6;
-    } else {
-      tr.streak = 0;
-    }
-  }
-  // ---- new tracks for unmatched detections, ids in ascending det order
-  // (rank among unmatched dets by a block prefix count)
+  // ---- bookkeeping (sort_tracker.py:234-276)
+  const int n_new = block_rank([&](int d) { return det_match[d] < 0; }, D, rank_d, wtot);
+  const int n_surv = block_rank(
+      [&](int t) {
+        const double upd = trk_match[t] >= 0 ? ts : tupd[t];
+        return (ts - upd) <= p.max_staleness;
+      },
+      T, rank_t, wtot);
+  // survivors keep their slots and their list order; unmatched tracks lose
+  // their hit streak
+  for (int q = tid; q < p.tmax; q += kAssocThreads) used[q] = 0;
   __syncthreads();
-  if (tid == 0) {
-    int r = 0;
-    for (int d = 0; d < D; ++d) {
-      if (det_match[d] < 0) {
-        keep_pos[p.tmax + d] = r;
-        ++r;
+  for (int t = tid; t < T; t += kAssocThreads) {
+    if (rank_t[t] >= 0) {
+      used[ord[t]] = 1;
+      ord_g[rank_t[t]] = ord[t];
+    }
+    if (trk_match[t] < 0) pl[ord[t]].streak = 0;
+  }
+  __syncthreads();
+  // new tracks (alive unless max_staleness < 0: last_update_ts = ts) take the
+  // free slots in ascending slot order, appended in detection order
+  const bool new_alive = 0.0 <= p.max_staleness;
+  const int room = p.tmax - n_surv;
+  const int n_fit = !new_alive ? 0 : (n_new < room ? n_new : room);
+  block_rank([&](int q) { return !used[q]; }, p.tmax, frank, wtot);
+  for (int q = tid; q < p.tmax; q += kAssocThreads) {
+    const int r = frank[q];
+    if (r >= 0 && r < n_fit) newslot[r] = q;
+  }
+  __syncthreads();
+  for (int r = tid; r < n_fit; r += kAssocThreads) ord_g[n_surv + r] = newslot[r];
+  // detection jobs for sort_update_kernel, {slot, id}: matched -> (its
+  // track's slot, -1); new -> (its slot, new id); new without room or pruned
+  // at once -> (-1, new id); no detection in the row -> (-2, -1)
+  for (int d = tid; d < p.dmax; d += kAssocThreads) {
+    int2 j = make_int2(-2, -1);
+    if (d < D) {
+      const int t = det_match[d];
+      if (t >= 0) {
+        j = make_int2(ord[t], -1);
       } else {
-        keep_pos[p.tmax + d] = -1;
+        const int r = rank_d[d];
+        j = make_int2(r < n_fit ? newslot[r] : -1, h.next_id + r);
       }
     }
-    s_cnt = r;
-  }
-  __syncthreads();
-  const int n_new = s_cnt;
-  bool overflow = T + n_new > p.tmax;
-  for (int d = tid; d < D; d += 256) {
-    const int r = keep_pos[p.tmax + d];
-    if (r < 0) continue;
-    const int slot = T + r;
-    if (slot >= p.tmax) {
-      oid[d] = h.next_id + r;  // id is consumed even though the track cannot be stored
-      continue;
-    }
-    Track& tr = Wk[slot];
-    track_init(tr, h.next_id + r, dd + d * 6, ts);
-    if (p.has_proj) {
-      const float* de = dd + d * 6;
-      update_metrics(p, tr, de[0], de[1], de[2], de[3], ts);
-      if (!isnone(tr.cur_dist)) odist[d] = tr.cur_dist;
-      if (!isnone(tr.cur_speed)) ospd[d] = tr.cur_speed * 3.6;
-    }
-    oid[d] = tr.id;
-  }
-  __syncthreads();
-  // ---- prune stale tracks: stable compaction work -> out, one lane per track
-  const int total = min(T + n_new, p.tmax);
-  if (tid == 0) {
-    int w = 0;
-    for (int t = 0; t < total; ++t) {
-      const bool alive = (ts - Wk[t].t_upd) <= p.max_staleness;
-      keep_pos[t] = alive ? w++ : -1;
-    }
-    s_cnt = w;
-  }
-  __syncthreads();
-  const int n_alive = s_cnt;
-  for (int t = tid; t < total; t += 256) {
-    const int dst = keep_pos[t];
-    if (dst < 0) continue;
-    const uint4* src4 = (const uint4*)&Wk[t];
-    uint4* dst4 = (uint4*)&T_out[dst];
-    for (int i = 0; i < (int)(sizeof(Track) / 16); ++i) dst4[i] = src4[i];
+    job[d] = j;
   }
   if (tid == 0) {
     StreamHdr o;
-    o.T = n_alive;
+    o.T = n_surv + n_fit;
     o.next_id = h.next_id + n_new;
-    o.overflow = h.overflow | (overflow ? 1 : 0);
+    o.overflow = h.overflow | (new_alive && n_new > room ? 1 : 0);
     o.pad = 0;
-    hout[s] = o;
+    hdr[s] = o;
   }
 }
 
-__global__ void sort_export_kernel(const StreamHdr* __restrict__ hdr, const Track* __restrict__ tr,
-                                   int tmax, double* __restrict__ x_out, int* __restrict__ meta,
+// One thread per detection row of every stream (sort_tracker.py:234-269).
+__global__ __launch_bounds__(256) void sort_update_kernel(
+    Track* __restrict__ pool, const float* __restrict__ dets, const double* __restrict__ ts_arr,
+    SortParams p, SortWs ws, int* __restrict__ out_id, double* __restrict__ out_dist,
+    double* __restrict__ out_speed) {
+  const int s = blockIdx.y;
+  const int d = blockIdx.x * 256 + threadIdx.x;
+  if (d >= p.dmax) return;
+  const size_t o = (size_t)s * p.dmax + d;
+  const int2 j = ws.det_job[o];
+  out_id[o] = -1;
+  out_dist[o] = NAN;
+  out_speed[o] = NAN;
+  if (j.x == -2) return;  // no detection
+  if (j.x < 0) {          // a new track that did not fit: the id is still consumed
+    out_id[o] = j.y;
+    return;
+  }
+  const float* de = dets + o * 6;
+  const double ts = ts_arr[s];
+  Track& tr = pool[(size_t)s * p.tmax + j.x];
+  if (j.y < 0) {  // matched: _Track.update + update_metrics
+    double z[4];
+    bbox_to_z(de[0], de[1], de[2], de[3], z);
+    kf_update(tr, z);
+    tr.t_pred = ts;
+    tr.t_upd = ts;
+    tr.hits += 1;
+    tr.streak += 1;
+    tr.cls = (int)de[5];
+    tr.conf = de[4];
+  } else {  // new track
+    track_init(tr, j.y, de, ts);
+  }
+  if (p.has_proj) update_metrics(p, tr, de[0], de[1], de[2], de[3], ts);
+  out_id[o] = tr.id;
+  if (p.has_proj) {
+    if (!isnone(tr.cur_dist)) out_dist[o] = tr.cur_dist;
+    if (!isnone(tr.cur_speed)) out_speed[o] = tr.cur_speed * 3.6;
+  }
+}
+
+// Per-stream state layout: headers (S x 16 B, padded to 256 B), the list
+// orders (S x tmax int32, padded), the track pools (S x tmax x Track).
+struct StateView {
+  StreamHdr* hdr;
+  int* order;
+  Track* pool;
+};
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static StateView state_view(const void* state, int S, int tmax) {
+  uint8_t* b = (uint8_t*)state;
+  StateView v;
+  v.hdr = (StreamHdr*)b;
+  b += align256((size_t)S * sizeof(StreamHdr));
+  v.order = (int*)b;
+  b += align256((size_t)S * tmax * sizeof(int));
+  v.pool = (Track*)b;
+  return v;
+}
+
+__global__ void sort_export_kernel(const StreamHdr* __restrict__ hdr, const int* __restrict__ order,
+                                   const Track* __restrict__ pool, int tmax,
+                                   double* __restrict__ x_out, int* __restrict__ meta,
                                    int* __restrict__ T_out) {
   const int s = blockIdx.x;
   const int T = hdr[s].T;
   if (threadIdx.x == 0) T_out[s] = T;
   for (int t = threadIdx.x; t < tmax; t += blockDim.x) {
-    const Track& k = tr[(size_t)s * tmax + t];
     const bool v = t < T;
+    const Track& k = pool[(size_t)s * tmax + (v ? order[(size_t)s * tmax + t] : 0)];
     for (int i = 0; i < 7; ++i) x_out[((size_t)s * tmax + t) * 7 + i] = v ? k.x[i] : 0.0;
     int* m = meta + ((size_t)s * tmax + t) * 4;
     m[0] = v ? k.id : -1;
@@ -517,17 +641,33 @@ using namespace rv;
 
 extern "C" size_t rv_sort_state_bytes(int S, int tmax) {
   if (S <= 0 || tmax <= 0) return 0;
-  return (((size_t)S * sizeof(StreamHdr) + 255) & ~(size_t)255) + (size_t)S * tmax * sizeof(Track);
+  return align256((size_t)S * sizeof(StreamHdr)) + align256((size_t)S * tmax * sizeof(int)) +
+         (size_t)S * tmax * sizeof(Track);
+}
+
+// M (argmax fallback) + predicted boxes + last_update_ts + detection jobs
+static size_t ws_parts(int S, int tmax, int dmax, size_t* off) {
+  size_t o = 0;
+  off[0] = o;
+  o = align256(o + (size_t)S * tmax * dmax * sizeof(float));
+  off[1] = o;
+  o = align256(o + (size_t)S * tmax * sizeof(float4));
+  off[2] = o;
+  o = align256(o + (size_t)S * tmax * sizeof(double));
+  off[3] = o;
+  o = align256(o + (size_t)S * dmax * sizeof(int2));
+  return o;
 }
 
 extern "C" size_t rv_sort_ws_bytes(int S, int tmax, int dmax) {
   if (S <= 0 || tmax <= 0 || dmax <= 0) return 0;
-  return (size_t)S * tmax * dmax * sizeof(float);
+  size_t off[4];
+  return ws_parts(S, tmax, dmax, off);
 }
 
 static size_t sort_smem(int tmax, int dmax) {
-  return (size_t)(tmax + dmax) * 16 + (size_t)kKeyCap * 8 + (size_t)(dmax + tmax) * 4 +
-         (size_t)(tmax + dmax) * 4;
+  return (size_t)(tmax + dmax) * 16 + (size_t)kKeyCap * 8 + (size_t)tmax * 8 +
+         (size_t)dmax * 4 * 3 + (size_t)tmax * 4 * 4 + (size_t)tmax;
 }
 
 extern "C" int rv_sort_init(void* state, int S, int tmax, void* stream) {
@@ -554,7 +694,7 @@ extern "C" int rv_sort_update(void* state_in, void* state_out, int S, int tmax,
                               const double* params6, const double* H9, const float* origin2,
                               void* ws, size_t ws_bytes, int* out_id, double* out_dist,
                               double* out_speed, void* stream) {
-  RV_CHECK_ARG(state_in && state_out && state_in != state_out, "state buffers must differ");
+  RV_CHECK_ARG(state_in && state_out, "null state");
   RV_CHECK_ARG(dets && dcount && ts && params6 && out_id && out_dist && out_speed && ws,
                "null pointer");
   RV_CHECK_ARG(S > 0 && tmax > 0 && tmax <= 8192 && dmax > 0 && dmax <= 4096, "bad sizes");
@@ -576,16 +716,18 @@ extern "C" int rv_sort_update(void* state_in, void* state_out, int S, int tmax,
     p.origin[0] = origin2[0];
     p.origin[1] = origin2[1];
   }
-  const size_t hb = ((size_t)S * sizeof(StreamHdr) + 255) & ~(size_t)255;
-  const StreamHdr* hin = (const StreamHdr*)state_in;
-  Track* tin = (Track*)((uint8_t*)state_in + hb);
-  StreamHdr* hout = (StreamHdr*)state_out;
-  Track* tout = (Track*)((uint8_t*)state_out + hb);
   const size_t smem = sort_smem(tmax, dmax);
   RV_CHECK_ARG(smem <= 160 * 1024, "tmax/dmax need %zu B of LDS", smem);
+  hipStream_t st = as_stream(stream);
+  int r = RV_OK;
+  if (state_out != state_in)  // the update runs in place on state_out
+    r = hip_check(hipMemcpyAsync(state_out, state_in, rv_sort_state_bytes(S, tmax),
+                                 hipMemcpyDeviceToDevice, st),
+                  "rv_sort_update state copy");
+  if (r) return r;
   static int attr_set = 0;
   if ((int)smem > attr_set) {  // once per growth, outside steady-state launches
-    hipError_t e = hipFuncSetAttribute((const void*)sort_update_kernel,
+    hipError_t e = hipFuncSetAttribute((const void*)sort_associate_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) {
       set_error("hipFuncSetAttribute(%zu B LDS): %s", smem, hipGetErrorString(e));
@@ -594,17 +736,33 @@ extern "C" int rv_sort_update(void* state_in, void* state_out, int S, int tmax,
     }
     attr_set = (int)smem;
   }
-  sort_update_kernel<<<S, 256, smem, as_stream(stream)>>>(hin, tin, hout, tout, dets, dcount, ts, p,
-                                                          (float*)ws, out_id, out_dist, out_speed);
-  return launch_status("rv_sort_update");
+  const StateView v = state_view(state_out, S, tmax);
+  size_t off[4];
+  ws_parts(S, tmax, dmax, off);
+  SortWs w;
+  w.M = (float*)((uint8_t*)ws + off[0]);
+  w.tbox = (float4*)((uint8_t*)ws + off[1]);
+  w.tupd = (double*)((uint8_t*)ws + off[2]);
+  w.det_job = (int2*)((uint8_t*)ws + off[3]);
+  sort_predict_kernel<<<dim3(ceil_div(tmax, 256), S), 256, 0, st>>>(v.hdr, v.order, v.pool, ts,
+                                                                     tmax, w);
+  r = launch_status("rv_sort_update (predict)");
+  if (r) return r;
+  sort_associate_kernel<<<S, kAssocThreads, smem, st>>>(v.hdr, v.order, v.pool, dets, dcount, ts, p,
+                                                       w);
+  r = launch_status("rv_sort_update (associate)");
+  if (r) return r;
+  sort_update_kernel<<<dim3(ceil_div(dmax, 256), S), 256, 0, st>>>(v.pool, dets, ts, p, w, out_id,
+                                                                   out_dist, out_speed);
+  return launch_status("rv_sort_update (update)");
 }
 
 extern "C" int rv_sort_export(const void* state, int S, int tmax, double* x_out, int* meta,
                               int* T_out, void* stream) {
   RV_CHECK_ARG(state && x_out && meta && T_out && S > 0 && tmax > 0, "bad args");
-  const size_t hb = ((size_t)S * sizeof(StreamHdr) + 255) & ~(size_t)255;
-  sort_export_kernel<<<S, 256, 0, as_stream(stream)>>>(
-      (const StreamHdr*)state, (const Track*)((const uint8_t*)state + hb), tmax, x_out, meta, T_out);
+  const StateView v = state_view(state, S, tmax);
+  sort_export_kernel<<<S, 256, 0, as_stream(stream)>>>(v.hdr, v.order, v.pool, tmax, x_out, meta,
+                                                       T_out);
   return launch_status("rv_sort_export");
 }
 

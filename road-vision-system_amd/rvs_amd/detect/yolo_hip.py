@@ -48,12 +48,18 @@ def class_mask(classes_keep: Sequence[int]) -> Optional[np.ndarray]:
 
 
 class YoloEngine:
-    """Batched letterbox -> YOLOv8 -> NMS for frames of one (H, W)."""
+    """Batched letterbox -> YOLOv8 -> NMS for frames of one (H, W).
+
+    `lanes` > 1 keeps that many independent forward contexts (plan handle +
+    activation workspace; the packed weights are shared), so forwards of
+    consecutive steps can run concurrently on different HIP streams -- each
+    forward is a latency-bound chain of small launches that leaves most of
+    the chip idle.  Letterbox and candidate buffers have 2 * lanes slots."""
 
     def __init__(self, variant: int, flat_weights: np.ndarray, max_batch: int, frame_hw,
                  imgsz: int = 640, stride: int = 32, conf: float = 0.25, iou: float = 0.7,
                  max_det: int = 100, classes_keep: Sequence[int] = (), max_wh: float = 7680.0,
-                 max_nms: int = 30000, device="cuda"):
+                 max_nms: int = 30000, device="cuda", lanes: int = 1):
         self.device = torch.device(device)
         self.variant = variant
         self.H, self.W = int(frame_hw[0]), int(frame_hw[1])
@@ -64,28 +70,36 @@ class YoloEngine:
         self.geo = kernels.letterbox_geometry(self.H, self.W, imgsz, stride)
         self.in_h, self.in_w = self.geo[0], self.geo[1]
         self.packed = torch.from_numpy(pack(variant, flat_weights)).to(self.device)
-        h = ctypes.c_void_p()
-        call("rv_yolo_create", variant, ptr(self.packed), self.max_batch, self.in_h, self.in_w,
-             ctypes.byref(h))
-        self._h = h
+        self.lanes = max(1, int(lanes))
+        self._hs = []
+        for _ in range(self.lanes):
+            h = ctypes.c_void_p()
+            call("rv_yolo_create", variant, ptr(self.packed), self.max_batch, self.in_h,
+                 self.in_w, ctypes.byref(h))
+            self._hs.append(h)
+        self._h = h = self._hs[0]
         lib = _lib.load()
         self.A = lib.rv_yolo_num_anchors(h)
         self.nc = 80
         self.ws_bytes = lib.rv_yolo_ws_bytes(h, self.max_batch)
         dev = self.device
-        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
-        # two letterbox slots: a pipelined engine letterboxes frame k+1 while
-        # the forward of frame k still reads its slot
-        self.lb = torch.empty((2, self.max_batch, self.in_h, self.in_w, 3), dtype=torch.uint8,
-                              device=dev)
+        self.wss = [torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
+                    for _ in range(self.lanes)]
+        self.ws = self.wss[0]
+        self.slots = 2 * self.lanes
+        # letterbox slots: a pipelined engine letterboxes frame k+1 while the
+        # forward(s) of earlier frames still read theirs
+        self.lb = torch.empty((self.slots, self.max_batch, self.in_h, self.in_w, 3),
+                              dtype=torch.uint8, device=dev)
         # segmented candidate layout: nseg segments of 64 rows per image
         self.nseg = lib.rv_yolo_cand_segments(h)
         self.cap = 64 * max(self.nseg, lib.rv_cand_segments(self.A))
-        # two candidate slots: a pipelined engine decodes frame k+1 into one
-        # slot while NMS still reads frame k's from the other
-        self.cand = torch.empty((2, self.max_batch, self.cap, CAND_BYTES // 4), dtype=torch.float32,
-                                device=dev)
-        self.seg_n = torch.zeros((2, self.max_batch, max(self.nseg, lib.rv_cand_segments(self.A))),
+        # candidate slots: a pipelined engine decodes frame k+1 into one slot
+        # while NMS still reads frame k's from another
+        self.cand = torch.empty((self.slots, self.max_batch, self.cap, CAND_BYTES // 4),
+                                dtype=torch.float32, device=dev)
+        self.seg_n = torch.zeros((self.slots, self.max_batch,
+                                  max(self.nseg, lib.rv_cand_segments(self.A))),
                                  dtype=torch.int32, device=dev)
         self.cand_n = torch.zeros(self.max_batch, dtype=torch.int32, device=dev)  # set by NMS
         # NMS workspace (sort keys of images with more than 4096 candidates)
@@ -100,9 +114,11 @@ class YoloEngine:
         self.keep = None if m is None else torch.from_numpy(m.view(np.int32)).to(dev)
 
     def close(self):
-        if self._h:
-            _lib.load().rv_yolo_destroy(self._h)
-            self._h = None
+        for h in getattr(self, "_hs", []):
+            if h:
+                _lib.load().rv_yolo_destroy(h)
+        self._hs = []
+        self._h = None
 
     def __del__(self):
         try:
@@ -114,20 +130,23 @@ class YoloEngine:
         """Raw forwards run the production kernel sequence (fused stem) when
         True, so forward_raw(raw) reproduces the candidate path's prediction
         exactly; False (default) keeps every activation for layer tests."""
-        call("rv_yolo_set_option", self._h, 1, 0 if fused else 1)
+        for h in self._hs:
+            call("rv_yolo_set_option", h, 1, 0 if fused else 1)
 
     def letterbox(self, frames: torch.Tensor, slot: int = 0) -> torch.Tensor:
         B = frames.shape[0]
         return kernels.letterbox(frames, self.geo, out=self.lb[slot][:B])
 
     def forward_raw(self, lb: torch.Tensor, raw: Optional[torch.Tensor] = None,
-                    candidates: bool = True, slot: int = 0):
-        """YOLOv8 forward + decode; candidates go to candidate slot `slot`."""
+                    candidates: bool = True, slot: int = 0, lane: int = 0):
+        """YOLOv8 forward + decode in forward context `lane`; candidates go to
+        candidate slot `slot`."""
         B = lb.shape[0]
         if B > self.max_batch:
             raise ValueError(f"batch {B} > max_batch {self.max_batch}")
         lb = lb.contiguous()
-        call("rv_yolo_forward", self._h, ptr(lb), B, ptr(self.ws), self.ws_bytes, ptr(raw),
+        call("rv_yolo_forward", self._hs[lane], ptr(lb), B, ptr(self.wss[lane]), self.ws_bytes,
+             ptr(raw),
              self.conf, ptr(self.cand[slot]) if candidates else None, self.cap,
              ptr(self.seg_n[slot]) if candidates else None, stream_ptr())
         self._nseg_cur = self.nseg
@@ -143,6 +162,11 @@ class YoloEngine:
         bad = ctypes.c_int(0)
         call("rv_yolo_autotune", self._h, ptr(lb), B, ptr(self.ws), self.ws_bytes, int(reps),
              1 if verify else 0, ctypes.byref(bad), stream_ptr())
+        if self.lanes > 1:  # the other forward contexts run the same plan
+            cfgs = self.tuned_configs()
+            for h in self._hs[1:]:
+                for i, c in enumerate(cfgs):
+                    call("rv_yolo_set_tuned", h, len(cfgs), i, _lib.int_array(c))
         return bad.value
 
     def tuned_configs(self):
@@ -160,8 +184,9 @@ class YoloEngine:
         """Install saved per-launch configurations (tuned_configs() of an
         earlier autotune of the same plan) instead of autotuning."""
         n = len(cfgs)
-        for i, c in enumerate(cfgs):
-            call("rv_yolo_set_tuned", self._h, n, i, _lib.int_array(c))
+        for h in self._hs:
+            for i, c in enumerate(cfgs):
+                call("rv_yolo_set_tuned", h, n, i, _lib.int_array(c))
 
     def nms(self, B: int, slot: int = 0):
         """NMS + scale_boxes + class filter of candidate slot `slot`."""

@@ -31,7 +31,7 @@ from .track.sort_hip import MultiStreamSort
 class RoadVisionEngine:
     def __init__(self, cfg: Optional[dict], n_streams: int, frame_hw, device="cuda",
                  tmax: int = 1024, projector: Optional[GroundProjector] = None,
-                 weights: Optional[np.ndarray] = None):
+                 weights: Optional[np.ndarray] = None, lanes: int = 1):
         cfg = cfg if cfg is not None else load_config()
         self.cfg = cfg
         self.S = int(n_streams)
@@ -46,7 +46,8 @@ class RoadVisionEngine:
             self.variant, weights, self.S, (self.H, self.W), imgsz=int(det_cfg.get("imgsz", 640)),
             conf=float(det_cfg.get("conf_thres", 0.25)), iou=float(det_cfg.get("iou_thres", 0.7)),
             max_det=int(det_cfg.get("max_det", 100)),
-            classes_keep=[int(x) for x in det_cfg.get("classes_keep", [])], device=self.device)
+            classes_keep=[int(x) for x in det_cfg.get("classes_keep", [])], device=self.device,
+            lanes=lanes)
         trk_cfg = cfg.get("tracking", {}) or {}
         self.tracker = MultiStreamSort(trk_cfg, self.S, tmax=tmax, dmax=self.detector.max_det,
                                        device=self.device)
@@ -74,9 +75,10 @@ class RoadVisionEngine:
         proc = self.pipeline(frames)
         return proc, self.detector.letterbox(proc, lb_slot)
 
-    def yolo_stage(self, lb: torch.Tensor, slot: int = 0) -> None:
-        """YOLOv8 forward + decode; NMS candidates land in candidate slot `slot`."""
-        self.detector.forward_raw(lb, slot=slot)
+    def yolo_stage(self, lb: torch.Tensor, slot: int = 0, lane: int = 0) -> None:
+        """YOLOv8 forward + decode in forward context `lane`; NMS candidates
+        land in candidate slot `slot`."""
+        self.detector.forward_raw(lb, slot=slot, lane=lane)
 
     def detect_stage(self, frames: torch.Tensor, slot: int = 0) -> torch.Tensor:
         proc, lb = self.preprocess_stage(frames)
@@ -184,7 +186,18 @@ class OverlappedSteps:
         """capture=False runs the same multi-stream schedule eagerly, right
         here (no graphs; run() is then a no-op): bench.py's per-launch conv
         timing uses it, since HIP events recorded inside captured graphs
-        do not time on ROCm 7.2 (measured: zero elapsed)."""
+        do not time on ROCm 7.2 (measured: zero elapsed).
+
+        With a detector of L >= 2 forward lanes (RoadVisionEngine(lanes=L))
+        the schedule is a dependency graph instead of lock-stepped stages:
+        P(j) on one stream, Y(j) on lane stream j % L, T(j) on one stream;
+        Y(j) waits for P(j) and for T(j - 2L) (its candidate slot), P(j) for
+        Y(j - 2L) (its letterbox slot), T(j) for Y(j) -- so the forwards of
+        L consecutive steps run concurrently while P runs ahead and T
+        follows; SORT still sees every stream's frames in order (the T
+        stages are one stream).  Each stage is its own captured graph and
+        run() replays them chained by HIP events (_issue); `chunk` does not
+        apply."""
         self.eng = eng
         ctx = (lambda g: torch.cuda.graph(g)) if capture else (lambda g: contextlib.nullcontext())
         K = len(frames)
@@ -194,10 +207,48 @@ class OverlappedSteps:
         self.outs = []
         self.records = [Record(eng.S, eng.detector.max_det, dev) for _ in range(K)]
         procs = {}
+        L = eng.detector.lanes
+        slots = eng.detector.slots
 
         def track(j):
-            o = eng.track_stage(ts[j], j % 2, self.records[j])
+            o = eng.track_stage(ts[j], j % slots, self.records[j])
             return {"record": o["record"]}
+        if chunk is None:
+            chunk = int(os.environ.get("RV_GRAPH_CHUNK", "8"))
+        self.staged = L > 1
+        if L > 1:
+            # Per-stage graphs chained by events at replay time (run()): a
+            # forward captured on a side stream of a multi-stream capture
+            # crashes hipStreamEndCapture on ROCm 7.2 (tools/probe_lanes.py),
+            # so every stage is captured alone on the capture stream and the
+            # dependency graph lives in the replay order + HIP events.
+            self.ys = [torch.cuda.Stream(dev) for _ in range(L)]
+            self.side_p, self.side_t = side_p, side_t
+            self.L, self.slots, self.K = L, slots, K
+            mk = (lambda: torch.cuda.Event()) if capture else (lambda: None)
+            self.eP = [mk() for _ in range(K)]
+            self.eY = [mk() for _ in range(K)]
+            self.eT = [mk() for _ in range(K)]
+            self.gP, self.gY, self.gT = [], [], []
+            if not capture:  # eager: the same chain, issued right here
+                self._issue(lambda j: eng.preprocess_stage(frames[j], j % slots),
+                            lambda j, lb: eng.yolo_stage(lb, j % slots, j % L),
+                            track, procs, events=False)
+                return
+            for j in range(K):
+                gp, gy, gt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gp):
+                    procs[j], lb = eng.preprocess_stage(frames[j], j % slots)
+                with torch.cuda.graph(gy):
+                    eng.yolo_stage(lb, j % slots, j % L)
+                with torch.cuda.graph(gt):
+                    out = track(j)
+                out["proc"] = procs.pop(j)
+                self.outs.append(out)
+                self.gP.append(gp)
+                self.gY.append(gy)
+                self.gT.append(gt)
+            return
         if depth == 2:
             for j in range(K + 1):
                 g = torch.cuda.CUDAGraph() if capture else None
@@ -223,8 +274,6 @@ class OverlappedSteps:
         # pipeline stages j are captured into one graph, so the device never
         # idles between graph replays inside a chunk; 0 = all K+2 stages in
         # one graph.  A serving loop replays one chunk per `chunk` steps.
-        if chunk is None:
-            chunk = int(os.environ.get("RV_GRAPH_CHUNK", "8"))
         js = list(range(-1, K + 1))
         size = len(js) if chunk <= 0 else chunk
         for c0 in range(0, len(js), size):
@@ -251,6 +300,50 @@ class OverlappedSteps:
             if capture:
                 self.graphs.append(g)
 
+    def _issue(self, P, Y, T, procs=None, events=True):
+        """The multi-lane chain: P(j) on side_p after Y(j - slots) (its
+        letterbox slot), Y(j) on lane stream j % L after P(j) and T(j - slots)
+        (its candidate slot), T(j) on side_t after Y(j); SORT sees the T's in
+        step order.  With graphs P / Y / T replay the captured stages; eager
+        (events=False) they run the stage functions and use fresh events."""
+        cur = torch.cuda.current_stream()
+        sp, st, ys = self.side_p, self.side_t, self.ys
+        for x in [sp, st] + ys:
+            x.wait_stream(cur)
+        eP, eY, eT = ((self.eP, self.eY, self.eT) if events else
+                      ([torch.cuda.Event() for _ in range(self.K)] for _ in range(3)))
+        S = self.slots
+        lbs = {}
+        for j in range(self.K):
+            ln = ys[j % self.L]
+            with torch.cuda.stream(sp):
+                if j >= S:
+                    sp.wait_event(eY[j - S])
+                r = P(j)
+                if procs is not None:
+                    procs[j], lbs[j] = r
+                eP[j].record(sp)
+            with torch.cuda.stream(ln):
+                ln.wait_event(eP[j])
+                if j >= S:
+                    ln.wait_event(eT[j - S])
+                Y(j, lbs.pop(j, None))
+                eY[j].record(ln)
+            with torch.cuda.stream(st):
+                st.wait_event(eY[j])
+                out = T(j)
+                eT[j].record(st)
+            if procs is not None:
+                out["proc"] = procs.pop(j)
+                self.outs.append(out)
+        for x in [sp, st] + ys:
+            cur.wait_stream(x)
+
     def run(self):
+        if self.staged:
+            if self.gP:
+                self._issue(lambda j: self.gP[j].replay(), lambda j, lb: self.gY[j].replay(),
+                            lambda j: self.gT[j].replay())
+            return
         for g in self.graphs:
             g.replay()

@@ -1,9 +1,12 @@
 """SORT on the GPU (drop-in for src/track/sort_tracker.py).
 
 ``MultiStreamSort`` keeps the state of S independent camera streams in HBM
-and advances all of them by one frame per call (rv_sort_update: one
-workgroup per stream; KF predict/update in f64, f32 IoU, greedy association
-identical to the reference's argmax loop, ground metrics).  ``SortTracker``
+(per stream: a pool of tmax track slots and the list order over them) and
+advances all of them by one frame per call, in place (rv_sort_update: KF
+predict over every track, one workgroup per stream for the association and
+bookkeeping, KF update / new tracks over every detection; f64 KF, f32 IoU,
+greedy association identical to the reference's argmax loop, ground
+metrics).  ``SortTracker``
 is the reference's single-stream ``Tracker.update(detections, timestamp,
 projector)`` on top of it, mutating and returning the same Detection objects
 (sort_tracker.py:212-278).
@@ -33,7 +36,7 @@ class MultiStreamSort:
         self.device = torch.device(device)
         lib = _lib.load()
         nb = lib.rv_sort_state_bytes(self.S, self.tmax)
-        self.state = [torch.empty(nb, dtype=torch.uint8, device=self.device) for _ in range(2)]
+        self.state = [torch.empty(nb, dtype=torch.uint8, device=self.device)]  # updated in place
         self.cur = 0
         self.ws_bytes = lib.rv_sort_ws_bytes(self.S, self.tmax, self.dmax)
         self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
@@ -65,13 +68,12 @@ class MultiStreamSort:
                            self.speed_window]
         if dets.shape[1] != self.dmax:
             raise ValueError(f"dets must be (S, {self.dmax}, 6)")
-        src, dst = self.state[self.cur], self.state[1 - self.cur]
+        st = self.state[0]
         Hp = self._H.ctypes.data if self._H is not None else None
         op = self._origin.ctypes.data if self._origin is not None else None
-        call("rv_sort_update", ptr(src), ptr(dst), self.S, self.tmax, ptr(dets), ptr(counts),
+        call("rv_sort_update", ptr(st), ptr(st), self.S, self.tmax, ptr(dets), ptr(counts),
              self.dmax, ptr(ts), self.params.ctypes.data, Hp, op, ptr(self.ws), self.ws_bytes,
              ptr(self.out_id), ptr(self.out_dist), ptr(self.out_speed), stream_ptr())
-        self.cur = 1 - self.cur
         return self.out_id, self.out_dist, self.out_speed
 
     def update_many(self, streams, timestamps) -> List[List[Detection]]:

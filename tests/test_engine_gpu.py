@@ -110,17 +110,20 @@ def test_results_record_matches_device_outputs(cuda):
     eng.close()
 
 
-@pytest.mark.parametrize("depth,chunk", [(2, None), (3, 1), (3, 3), (3, None), (3, 0)])
-def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk):
+@pytest.mark.parametrize("depth,chunk,lanes", [(2, None, 1), (3, 1, 1), (3, 3, 1), (3, None, 1),
+                                               (3, 0, 1), (3, None, 2), (3, 3, 2), (3, 0, 3)])
+def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk, lanes):
     """bench.py's timed mode (engine.OverlappedSteps): the track stage of step
     k runs on a side stream beside the preprocess of step k+1, with `chunk`
-    pipeline stages per captured graph (None = the default 8, 0 = one graph).
-    EVERY step's handed-back detections / track ids and proc frames, and the
-    final SORT state, must equal those of plain sequential step() calls."""
+    pipeline stages per captured graph (None = the default 8, 0 = one graph);
+    lanes >= 2: the dependency-graph schedule with that many concurrent YOLO
+    forwards.  EVERY step's handed-back detections / track ids and proc
+    frames, and the final SORT state, must equal those of plain sequential
+    step() calls."""
     from rvs_amd.engine import OverlappedSteps, RoadVisionEngine
     from rvs_amd.synth import road_frames
     cfg = _cfg()
-    S, H, W, F = 4, 1080, 1920, 6
+    S, H, W, F = 4, 1080, 1920, 8
     frames = road_frames(S, F, H, W, device=cuda)
     ts = torch.tensor([[f / 30.0] * S for f in range(F)], dtype=torch.float64, device=cuda)
     seq = RoadVisionEngine(cfg, S, (H, W), device=cuda)
@@ -129,7 +132,7 @@ def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk):
         out_seq = seq.step(frames[f], ts[f])
         seq_res.append(seq.results(out_seq))
         seq_proc.append(out_seq["proc"].cpu().numpy())
-    ovl = RoadVisionEngine(cfg, S, (H, W), device=cuda)
+    ovl = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=lanes)
     ovl.step(frames[0], ts[0])  # eager first step (one-time kernel setup)
     run = OverlappedSteps(ovl, [frames[f] for f in range(1, F)], [ts[f] for f in range(1, F)],
                           depth=depth, chunk=chunk)
@@ -151,7 +154,8 @@ def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk):
     ovl.close()
 
 
-def test_bench_configuration_parity(cuda):
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_bench_configuration_parity(cuda, lanes):
     """Exactly bench.py's timed configuration (S = 32 streams of 1080p,
     autotuned conv kernels, OverlappedSteps(depth=3, chunk=8), hand-back
     into per-step host records), checked against the oracle on every step:
@@ -162,7 +166,7 @@ def test_bench_configuration_parity(cuda):
     from rvs_amd.synth import road_frames
     cfg = _cfg()
     S, H, W, WARM, K = 32, 1080, 1920, 2, 8
-    eng = RoadVisionEngine(cfg, S, (H, W), device=cuda)
+    eng = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=lanes)
     frames = road_frames(S, WARM + K, H, W, device=cuda)
     ts = torch.tensor([[f / 30.0] * S for f in range(WARM + K)], dtype=torch.float64, device=cuda)
     chk = Checker(eng, cfg, proc_streams=[0, 13, 31])
