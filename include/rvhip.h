@@ -154,9 +154,15 @@ int rv_yolo_create(int variant, const void* dev_packed, int max_B, int in_h, int
 int rv_yolo_destroy(void* handle);
 /* Handle options.  RV_YOLO_OPT_RAW_UNFUSED (default 1): a forward asked for
  * raw_out runs the unfused stem, so the P1 map (X0) lands in the workspace
- * for layer-wise inspection; 0: raw forwards run the production kernel
- * sequence (fused stem), so raw_out is what the candidate path computed. */
+ * for layer-wise inspection (and the C2f blocks unfused); 0: raw forwards
+ * run the production kernel sequence, so raw_out is what the candidate
+ * path computed. */
 #define RV_YOLO_OPT_RAW_UNFUSED 1
+/* RV_YOLO_OPT_FUSE_C2F (default 1): the narrow C2f blocks (hidden width 16
+ * or 32: YOLOv8n model.2 / model.4 / model.15) run as cv1 + one fused
+ * launch for the bottlenecks and cv2 (bit-identical to the unfused convs);
+ * 0: one launch per conv. */
+#define RV_YOLO_OPT_FUSE_C2F 2
 int rv_yolo_set_option(void* handle, int opt, int value);
 size_t rv_yolo_ws_bytes(void* handle, int B);
 int rv_yolo_num_anchors(void* handle);

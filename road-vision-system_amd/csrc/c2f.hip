@@ -1,0 +1,330 @@
+// Fused C2f bottleneck chain + cv2 for the narrow (C <= 32) C2f blocks of
+// YOLOv8 (Ultralytics C2f / Bottleneck; oracle/yolo_ref.py YoloRef.c2f):
+//
+//   y0, y1 = cv1(x).chunk(2)          (cv1 runs before, as a normal 1x1 conv,
+//                                      into the block's concat buffer)
+//   z_i = [y_in +] cvb_i(cva_i(y_in))  (3x3 C -> C twice, residual if shortcut;
+//                                      y_in = y1 for i = 0, z_{i-1} after)
+//   out = cv2(cat(y0, y1, z_0 .. z_{N-1}))   (1x1 (2+N)C -> 2C)
+//
+// One workgroup (8 waves) per TR x TC output tile of one image.  y1 is read
+// with a halo of 2N pixels (each 3x3 conv eats one), y0 at the tile only;
+// every intermediate (t_i = cva_i(.), z_i) lives in LDS only and never
+// touches HBM -- the unfused form writes and re-reads all of them, one
+// launch per conv.  Out-of-image pixels of every LDS map are zero (the next
+// 3x3 conv's padding).
+//
+// Bit-identical to the unfused kernels (conv_patch_kernel /
+// conv1x1_direct_kernel): the same v_mfma_f32_16x16x32_bf16 k-order (taps
+// (ky, kx) ascending with one 32-channel k-step each -- channels >= C are
+// zero in both operands -- and cv2's 32-channel chunks ascending), the same
+// epilogue (bias, SiLU, residual add of the bf16 input, round to bf16).
+//
+// LDS maps are pixel-major, PB = 2C bytes per pixel (C channels of bf16),
+// 16-B quarters XOR-swizzled by pixel index so the 16 pixels of a fragment
+// hit disjoint bank groups.
+#include "conv.h"
+
+namespace rv {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8c;
+typedef __attribute__((ext_vector_type(4))) float f32x4c;
+typedef __attribute__((ext_vector_type(2))) float f32x2c;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2c;
+
+__device__ __forceinline__ uint32_t c2f_pack(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2c{lo, hi}, bf16x2c));
+}
+__device__ __forceinline__ float c2f_bf2f(uint32_t h) { return __uint_as_float(h << 16); }
+__device__ __forceinline__ float c2f_silu(float v) {
+  return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+}
+
+template <int C>
+struct C2fGeo {
+  static constexpr int PB = 2 * C;      // bytes per pixel
+  static constexpr int NQ = PB / 16;    // 16-B quarters per pixel
+  static constexpr int MR = C / 16;     // 16-cout fragments of a C-out conv
+  // physical quarter of logical quarter q of pixel p
+  __device__ static __forceinline__ int swz(int p, int q) {
+    return NQ == 4 ? (q ^ ((p >> 2) & 3)) : (q ^ ((p >> 3) & 1));
+  }
+  __device__ static __forceinline__ int addr(int p, int q) { return p * PB + (swz(p, q) << 4); }
+};
+
+template <int TR, int TC>
+struct C2fTile {
+  __host__ __device__ static constexpr int rh(int e) { return TR + 2 * e; }
+  __host__ __device__ static constexpr int rw(int e) { return TC + 2 * e; }
+  __host__ __device__ static constexpr int rp(int e) { return rh(e) * rw(e); }
+};
+
+template <int C, int N, int TR, int TC>
+struct C2fLds {
+  using G = C2fGeo<C>;
+  using T = C2fTile<TR, TC>;
+  static constexpr int h = 2 * N;
+  static constexpr int Y = 0;                                  // y1, halo h
+  static constexpr int Tb = Y + T::rp(h) * G::PB;              // t_i (largest: halo h-1)
+  static constexpr int Z0 = Tb + T::rp(h - 1) * G::PB;         // z_0, halo h-2
+  static constexpr int Z1 = Z0 + T::rp(h - 2) * G::PB;         // z_1, halo h-4 (N = 2)
+  static constexpr int Y0 = Z1 + (N == 2 ? T::rp(0) * G::PB : 0);  // y0, halo 0
+  static constexpr int BYTES = Y0 + T::rp(0) * G::PB;
+};
+
+// 3x3 C -> C conv from an LDS map at halo e_out + 1 into one at halo e_out
+// (+ residual from an LDS map at halo e_res), zero outside the image.
+template <int C, int TR, int TC, bool RES>
+__device__ __forceinline__ void c2f_conv3(const uint8_t* __restrict__ in, uint8_t* __restrict__ outb,
+                                          int e_out, const bf16_t* __restrict__ w,
+                                          const float* __restrict__ bias,
+                                          const uint8_t* __restrict__ res, int e_res, int oy0,
+                                          int ox0, int H, int W) {
+  using G = C2fGeo<C>;
+  using T = C2fTile<TR, TC>;
+  constexpr int MR = G::MR;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int col = lane & 15, quad = lane >> 4;
+  const int rwo = T::rw(e_out), rpo = T::rp(e_out), rwi = rwo + 2, rwr = T::rw(e_res);
+  // A fragments of all 9 taps: packed [Cout_pad16][3][3][32] (Cin zero-padded to 32)
+  bf16x8c A[9][MR];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+      A[t][m] = __builtin_bit_cast(bf16x8c,
+                                   *(const uint4*)(w + ((size_t)(m * 16 + col) * 9 + t) * 32 + quad * 8));
+  f32x4c bv[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) bv[m] = *(const f32x4c*)(bias + m * 16 + quad * 4);
+  const int nfrag = (rpo + 15) / 16;
+  for (int f0 = wave * 2; f0 < nfrag; f0 += 16) {
+    f32x4c acc[2][MR];
+    int base[2], o[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      o[n] = (f0 + n) * 16 + col;
+      const int oo = o[n] < rpo ? o[n] : 0;
+      const int r = oo / rwo, c = oo - r * rwo;
+      base[n] = r * rwi + c;
+#pragma unroll
+      for (int m = 0; m < MR; ++m) acc[n][m] = f32x4c{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int p = base[n] + ky * rwi + kx;
+          uint4 b = make_uint4(0, 0, 0, 0);
+          if (quad < G::NQ) b = *(const uint4*)(in + G::addr(p, quad));
+          const bf16x8c B = __builtin_bit_cast(bf16x8c, b);
+#pragma unroll
+          for (int m = 0; m < MR; ++m)
+            acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ky * 3 + kx][m], B, acc[n][m], 0, 0, 0);
+        }
+      }
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      if (o[n] >= rpo) continue;
+      const int r = o[n] / rwo, c = o[n] - (o[n] / rwo) * rwo;
+      const int gy = oy0 - e_out + r, gx = ox0 - e_out + c;
+      const bool inside = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = c2f_silu(acc[n][m][i] + bv[m][i]);
+        const int lq = (m * 16 + quad * 4) >> 3, half = (quad & 1) * 8;
+        if (RES) {
+          const int d = e_res - e_out;
+          const int pr = (r + d) * rwr + c + d;
+          const uint2 rr = *(const uint2*)(res + G::addr(pr, lq) + half);
+          v[0] += c2f_bf2f(rr.x & 0xFFFF);
+          v[1] += c2f_bf2f(rr.x >> 16);
+          v[2] += c2f_bf2f(rr.y & 0xFFFF);
+          v[3] += c2f_bf2f(rr.y >> 16);
+        }
+        const uint2 pk = inside ? make_uint2(c2f_pack(v[0], v[1]), c2f_pack(v[2], v[3]))
+                                : make_uint2(0, 0);
+        *(uint2*)(outb + G::addr(o[n], lq) + half) = pk;
+      }
+    }
+  }
+}
+
+template <int C, int N, bool SC, int TR, int TC>
+__global__ __launch_bounds__(512) void c2f_chain_kernel(C2fArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  using G = C2fGeo<C>;
+  using T = C2fTile<TR, TC>;
+  using L = C2fLds<C, N, TR, TC>;
+  constexpr int h = 2 * N;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int col = lane & 15, quad = lane >> 4;
+  const int tiles_x = (a.W + TC - 1) / TC, tiles_y = (a.H + TR - 1) / TR;
+  int bid = blockIdx.x;
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int b = bid / tiles_y;
+  const int oy0 = ty * TR, ox0 = tx * TC;
+  const bf16_t* img = a.cat + (size_t)b * a.H * a.W * a.cat_cs + a.cat_co;
+
+  // ---- 1. y1 (halo h) and y0 (tile) from the concat buffer, zero outside
+  {
+    constexpr int NY = T::rp(h) * G::NQ, N0 = T::rp(0) * G::NQ;
+    constexpr int NT = NY + N0;
+    constexpr int IT = 4;  // loads in flight per thread
+    for (int i0 = tid; i0 < NT; i0 += 512 * IT) {
+      uint4 v[IT];
+      int dst[IT];
+#pragma unroll
+      for (int u = 0; u < IT; ++u) {
+        const int i = i0 + u * 512;
+        v[u] = make_uint4(0, 0, 0, 0);
+        dst[u] = -1;
+        if (i < NT) {
+          const bool is1 = i < NY;
+          const int j = is1 ? i : i - NY;
+          const int p = j / G::NQ, q = j - p * G::NQ;
+          const int e = is1 ? h : 0;
+          const int rwe = T::rw(e);
+          const int r = p / rwe, c = p - r * rwe;
+          const int gy = oy0 - e + r, gx = ox0 - e + c;
+          dst[u] = (is1 ? L::Y : L::Y0) + G::addr(p, q);
+          if ((unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W)
+            v[u] = *(const uint4*)(img + ((size_t)gy * a.W + gx) * a.cat_cs + (is1 ? C : 0) + q * 8);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < IT; ++u)
+        if (dst[u] >= 0) *(uint4*)(smem + dst[u]) = v[u];
+    }
+  }
+  __syncthreads();
+
+  // ---- 2. bottlenecks: t = cva(y_in) at halo e-1, z = [y_in +] cvb(t) at e-2
+  c2f_conv3<C, TR, TC, false>(smem + L::Y, smem + L::Tb, h - 1, a.wa[0], a.ba[0], nullptr, 0, oy0,
+                              ox0, a.H, a.W);
+  __syncthreads();
+  c2f_conv3<C, TR, TC, SC>(smem + L::Tb, smem + L::Z0, h - 2, a.wb[0], a.bb[0], smem + L::Y, h, oy0,
+                           ox0, a.H, a.W);
+  __syncthreads();
+  if constexpr (N == 2) {
+    c2f_conv3<C, TR, TC, false>(smem + L::Z0, smem + L::Tb, h - 3, a.wa[1], a.ba[1], nullptr, 0, oy0,
+                                ox0, a.H, a.W);
+    __syncthreads();
+    c2f_conv3<C, TR, TC, SC>(smem + L::Tb, smem + L::Z1, h - 4, a.wb[1], a.bb[1], smem + L::Z0, h - 2,
+                             oy0, ox0, a.H, a.W);
+    __syncthreads();
+  }
+
+  // ---- 3. cv2: 1x1 over cat(y0, y1, z_0 .. z_{N-1}) at the tile -> HBM
+  constexpr int KC = (2 + N) * C;        // concat channels
+  constexpr int NCH = (KC + 31) / 32;    // 32-channel k-steps
+  constexpr int MR2 = 2 * C / 16;        // cv2 cout fragments (2C couts)
+  constexpr int KP = NCH * 32;           // packed Cin (padded to 32)
+  bf16x8c A2[NCH][MR2];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int m = 0; m < MR2; ++m)
+      A2[j][m] = __builtin_bit_cast(bf16x8c,
+                                    *(const uint4*)(a.w2 + (size_t)(m * 16 + col) * KP + j * 32 + quad * 8));
+  f32x4c bv2[MR2];
+#pragma unroll
+  for (int m = 0; m < MR2; ++m) bv2[m] = *(const f32x4c*)(a.b2 + m * 16 + quad * 4);
+  // segment s of the concat: 0 = y0 (halo 0), 1 = y1 (halo h), 2 + i = z_i
+  auto seg_buf = [&](int s) -> int {
+    return s == 0 ? L::Y0 : (s == 1 ? L::Y : (s == 2 ? L::Z0 : L::Z1));
+  };
+  auto seg_halo = [&](int s) -> int { return s == 0 ? 0 : (s == 1 ? h : h - 2 * (s - 1)); };
+  constexpr int RP0 = T::rp(0);
+  constexpr int NFR = RP0 / 16;
+  for (int f0 = wave * 2; f0 < NFR; f0 += 16) {
+    f32x4c acc[2][MR2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int m = 0; m < MR2; ++m) acc[n][m] = f32x4c{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int k0 = j * 32 + quad * 8;  // first concat channel of this lane's k-slice
+      const int s = k0 / C, qq = (k0 - s * C) >> 3;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int o = (f0 + n) * 16 + col;
+        const int r = o / TC, c = o - (o / TC) * TC;
+        uint4 bq = make_uint4(0, 0, 0, 0);
+        if (s < 2 + N) {
+          const int e = seg_halo(s);
+          const int p = (r + e) * T::rw(e) + c + e;
+          bq = *(const uint4*)(smem + seg_buf(s) + G::addr(p, qq));
+        }
+        const bf16x8c B = __builtin_bit_cast(bf16x8c, bq);
+#pragma unroll
+        for (int m = 0; m < MR2; ++m)
+          acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2[j][m], B, acc[n][m], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int o = (f0 + n) * 16 + col;
+      const int r = o / TC, c = o - (o / TC) * TC;
+      const int gy = oy0 + r, gx = ox0 + c;
+      if (gy >= a.H || gx >= a.W) continue;
+      uint16_t* dst = a.out + ((size_t)(b * a.H + gy) * a.W + gx) * a.out_cs + a.out_co;
+#pragma unroll
+      for (int m = 0; m < MR2; ++m) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = c2f_silu(acc[n][m][i] + bv2[m][i]);
+        *(uint2*)(dst + m * 16 + quad * 4) = make_uint2(c2f_pack(v[0], v[1]), c2f_pack(v[2], v[3]));
+      }
+    }
+  }
+}
+
+template <int C, int N, bool SC, int TR, int TC>
+static int launch_c2f_t(const C2fArgs& a, hipStream_t s) {
+  using L = C2fLds<C, N, TR, TC>;
+  static_assert(L::BYTES <= 160 * 1024, "C2f tile exceeds LDS");
+  static_assert((TR * TC) % 32 == 0, "tile must hold whole fragment pairs");
+  auto fn = c2f_chain_kernel<C, N, SC, TR, TC>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       L::BYTES);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      set_error("hipFuncSetAttribute(c2f): %s", hipGetErrorString(e));
+      return -(int)e;
+    }
+    attr = true;
+  }
+  const int blocks = a.B * ceil_div(a.H, TR) * ceil_div(a.W, TC);
+  fn<<<blocks, 512, L::BYTES, s>>>(a);
+  return launch_status("c2f_chain");
+}
+
+bool c2f_fusable(int C, int N, int cat_cs, int cat_co, int out_cs, int out_co) {
+  return (C == 16 || C == 32) && (N == 1 || N == 2) && !(C == 16 && N == 2) && cat_cs % 8 == 0 &&
+         cat_co % 8 == 0 && out_cs % 4 == 0 && out_co % 4 == 0;
+}
+
+int launch_c2f_chain(const C2fArgs& a, int C, int N, bool shortcut, hipStream_t s) {
+  if (!c2f_fusable(C, N, a.cat_cs, a.cat_co, a.out_cs, a.out_co)) {
+    set_error("c2f_chain: C=%d N=%d unsupported", C, N);
+    return RV_EINVAL;
+  }
+  // tiles: 16 x 32 at C = 16 (P2 maps), 16 x 16 at C = 32 (P3 maps divide)
+  if (C == 16) return shortcut ? launch_c2f_t<16, 1, true, 16, 32>(a, s)
+                               : launch_c2f_t<16, 1, false, 16, 32>(a, s);
+  if (N == 1) return shortcut ? launch_c2f_t<32, 1, true, 16, 16>(a, s)
+                              : launch_c2f_t<32, 1, false, 16, 16>(a, s);
+  return shortcut ? launch_c2f_t<32, 2, true, 16, 16>(a, s) : launch_c2f_t<32, 2, false, 16, 16>(a, s);
+}
+
+}  // namespace rv

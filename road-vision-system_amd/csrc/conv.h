@@ -38,6 +38,9 @@ struct ConvArgs {
   int g2_cout0, g2_in_co, g2_Cin;
   const bf16_t* g2_w;
   const float* g2_bias;
+  // > 0: this launch record stands for a fused C2f chain (yolo.hip's
+  // Model::fused[fused - 1]); the autotuner leaves it alone
+  int fused;
 };
 
 // One configuration of the LDS-staged conv kernel: MR x NR 16x16 fragments
@@ -73,6 +76,27 @@ int launch_stem(const uint8_t* img, int B, int H, int W, const float* w0, const 
 // SPPF pooling: buf holds x in channels [0, c); writes maxpool5, maxpool5^2
 // and maxpool5^3 (= clipped 5/9/13 windows) into [c,2c), [2c,3c), [3c,4c).
 int launch_sppf_pool(bf16_t* buf, int B, int H, int W, int c, hipStream_t s);
+
+// Fused C2f bottleneck chain + cv2 (c2f.hip) for C2f blocks with hidden
+// width C in {16, 32} and N in {1, 2} bottlenecks (C = 16: N = 1): reads
+// y0 / y1 (cv1's output, channels [cat_co, cat_co + 2C) of the block's
+// concat buffer), writes cv2's 2C channels to the output view.  Every
+// intermediate stays in LDS.  Bit-identical to the unfused launches.
+struct C2fArgs {
+  const bf16_t* cat;
+  int cat_cs, cat_co;
+  int H, W, B;
+  const bf16_t* wa[2];
+  const float* ba[2];
+  const bf16_t* wb[2];
+  const float* bb[2];
+  const bf16_t* w2;
+  const float* b2;
+  bf16_t* out;
+  int out_cs, out_co;
+};
+bool c2f_fusable(int C, int N, int cat_cs, int cat_co, int out_cs, int out_co);
+int launch_c2f_chain(const C2fArgs& a, int C, int N, bool shortcut, hipStream_t s);
 
 struct HeadLevel {
   const float* logits;  // [B][H][W][cs] f32: [0,4*reg) box bins, [4*reg, 4*reg+nc) classes

@@ -195,6 +195,12 @@ struct Model {
   std::vector<TraceRec> trace;  // conv specs run by the last forward (one record each)
   std::vector<ConvArgs> launches;  // conv kernel launches of the last forward
   std::vector<ConvCfg> tuned;      // per launch index: autotuned config (mr 0 = default)
+  struct FusedC2f {
+    C2fArgs a;
+    int C, N;
+    bool shortcut;
+  };
+  std::vector<FusedC2f> fused;     // fused C2f chains of the last forward (ConvArgs::fused)
   std::vector<std::pair<std::string, int>> tmps;  // bottleneck temp buffer per "prefix.m.i"
   int tmp_of(const std::string& k) const {
     for (auto& t : tmps)
@@ -217,6 +223,8 @@ struct Model {
   // RV_YOLO_OPT_RAW_UNFUSED: forwards that return the raw prediction run the
   // unfused stem, so every activation (X0 included) is in the workspace
   int raw_unfused = 1;
+  // RV_YOLO_OPT_FUSE_C2F: narrow C2f blocks as cv1 + one fused chain launch
+  int fuse_c2f = 1;
   std::vector<Buf> bufs;
   int nA = 0;
   int map_h[6], map_w[6];  // stride 2^i maps
@@ -413,20 +421,26 @@ struct Exec {
         rec ? hip_check(hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + li_) * 2], s),
                         "profile hipEventRecord")
             : RV_OK;
-    if (li_ < (int)M->tuned.size() && M->tuned[li_].mr > 0 && conv_cfg_ok(a, M->tuned[li_]))
+    if (a.fused > 0) {
+      const Model::FusedC2f& f = M->fused[a.fused - 1];
+      status = launch_c2f_chain(f.a, f.C, f.N, f.shortcut, s);
+    } else if (li_ < (int)M->tuned.size() && M->tuned[li_].mr > 0 &&
+               conv_cfg_ok(a, M->tuned[li_])) {
       status = launch_conv_cfg(a, M->tuned[li_], s);
-    else
+    } else {
       status = launch_conv(a, s);
+    }
     if (!status) status = ev0;
     if (rec && !status)
       status = hip_check(hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + li_) * 2 + 1], s),
                          "profile hipEventRecord");
     if (P.on && P.n_fwd == 0 && li_ < P.per_fwd) {
       P.flops[li_] = flops;
-      P.bytes[li_] = launch_bytes(a);
+      P.bytes[li_] = a.fused > 0 ? fused_bytes : launch_bytes(a);
       P.conv_of[li_] = idx;
     }
   }
+  double fused_bytes = 0.0;  // algorithmic bytes of the next fused launch
 
   // conv `name`: input view at map level li -> up to two output views
   void conv(const std::string& name, View in, int li, View o0, int up0 = 0, View o1 = {-1, 0, 0},
@@ -474,12 +488,72 @@ struct Exec {
     launch(a, i1, fl);
   }
 
-  // C2f(prefix): in view (map li) -> concat buffer cb -> outputs
+  // C2f(prefix): in view (map li) -> concat buffer cb -> outputs.  With
+  // `fuse`, narrow blocks run cv1 and then one fused launch for the
+  // bottlenecks + cv2 (c2f.hip; intermediates stay in LDS).
   void c2f(const std::string& p, View in, int li, int cb, int c2, int n, bool shortcut, View o0,
-           int up0 = 0, View o1 = {-1, 0, 0}, int up1 = 0) {
+           int up0 = 0, View o1 = {-1, 0, 0}, int up1 = 0, bool fuse = false) {
     const int c = c2 / 2;
     const int cs = (2 + n) * c;
     conv(p + ".cv1", in, li, View{cb, cs, 0});
+    if (fuse && !status && up0 == 0 && o1.buf < 0 && c2f_fusable(c, n, cs, 0, o0.cs, o0.co)) {
+      Model::FusedC2f f;
+      memset(&f.a, 0, sizeof(f.a));
+      f.C = c;
+      f.N = n;
+      f.shortcut = shortcut;
+      f.a.cat = (const bf16_t*)ptr(cb);
+      f.a.cat_cs = cs;
+      f.a.cat_co = 0;
+      f.a.H = M->map_h[li];
+      f.a.W = M->map_w[li];
+      f.a.B = B;
+      double flops = 0.0;
+      ConvArgs rec;
+      for (int i = 0; i < n; ++i) {
+        const std::string q = p + ".m." + std::to_string(i);
+        const int ia = spec(q + ".cv1"), ib = spec(q + ".cv2");
+        if (ia < 0 || ib < 0) return;
+        const ConvSpec& ca = M->def.convs[ia];
+        const ConvSpec& cbv = M->def.convs[ib];
+        f.a.wa[i] = wptr(ca);
+        f.a.ba[i] = bptr(ca);
+        f.a.wb[i] = wptr(cbv);
+        f.a.bb[i] = bptr(cbv);
+        // trace records keep the layer list complete (the buffers are not
+        // written: parity forwards run unfused)
+        const int tmp = M->tmp_of(q);
+        const View bin{cb, cs, (1 + i) * c};
+        const View none{-1, 0, 0};
+        ConvArgs aa = args(ca, bin, li, View{tmp, c, 0}, 0, none, 0, none);
+        trace(ia, aa, bin, View{tmp, c, 0}, 0, none, 0, none);
+        ConvArgs ab = args(cbv, View{tmp, c, 0}, li, View{cb, cs, (2 + i) * c}, 0, none, 0,
+                           shortcut ? bin : none);
+        trace(ib, ab, View{tmp, c, 0}, View{cb, cs, (2 + i) * c}, 0, none, 0, shortcut ? bin : none);
+        flops += flops_of(ca, aa) + flops_of(cbv, ab);
+      }
+      const int i2 = spec(p + ".cv2");
+      if (i2 < 0) return;
+      const ConvSpec& c2s = M->def.convs[i2];
+      f.a.w2 = wptr(c2s);
+      f.a.b2 = bptr(c2s);
+      f.a.out = (bf16_t*)ptr(o0.buf);
+      f.a.out_cs = o0.cs;
+      f.a.out_co = o0.co;
+      rec = args(c2s, View{cb, cs, 0}, li, o0, 0, View{-1, 0, 0}, 0, View{-1, 0, 0});
+      trace(i2, rec, View{cb, cs, 0}, o0, 0, View{-1, 0, 0}, 0, View{-1, 0, 0});
+      flops += flops_of(c2s, rec);
+      M->fused.push_back(f);
+      rec.fused = (int)M->fused.size();
+      // algorithmic bytes: y0 + y1 read once, cv2's output written once,
+      // every weight of the chain read once
+      double wbytes = 0.0;
+      for (int i = 0; i < n; ++i) wbytes += 2.0 * 2 * 9 * c * 32;
+      wbytes += 2.0 * c2 * ((cs + 31) / 32 * 32);
+      fused_bytes = (double)B * f.a.H * f.a.W * (2.0 * c * 2 + 2.0 * c2) + wbytes;
+      launch(rec, i2, flops);
+      return;
+    }
     for (int i = 0; i < n; ++i) {
       const View bin{cb, cs, (1 + i) * c};
       const std::string q = p + ".m." + std::to_string(i);
@@ -604,6 +678,9 @@ extern "C" int rv_yolo_set_option(void* h, int opt, int value) {
     case RV_YOLO_OPT_RAW_UNFUSED:
       M->raw_unfused = value != 0;
       return RV_OK;
+    case RV_YOLO_OPT_FUSE_C2F:
+      M->fuse_c2f = value != 0;
+      return RV_OK;
     default:
       set_error("unknown yolo option %d", opt);
       return RV_EINVAL;
@@ -649,6 +726,7 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   }
   M->trace.clear();
   M->launches.clear();
+  M->fused.clear();
   // backbone
   const ConvSpec& c0 = M->def.convs[0];
   // conv0 + model.1 fused (the P1 map stays in LDS) unless the caller asked
@@ -675,12 +753,17 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
     if (st) return st;
     E.conv("model.1", View{M->X0, v.c1, 0}, 1, View{M->X1, v.c2, 0});
   }
-  E.c2f("model.2", View{M->X1, v.c2, 0}, 2, M->C2, v.c2, v.nb, true, View{M->X2, v.c2, 0});
+  // fused C2f chains (c2f.hip) unless a raw parity forward keeps every
+  // activation (RV_YOLO_OPT_RAW_UNFUSED) or RV_FUSE_C2F=0
+  static const bool c2f_env = !getenv("RV_FUSE_C2F") || atoi(getenv("RV_FUSE_C2F")) != 0;
+  const bool fuse_c2f = c2f_env && M->fuse_c2f && !(raw_out && M->raw_unfused);
+  E.c2f("model.2", View{M->X1, v.c2, 0}, 2, M->C2, v.c2, v.nb, true, View{M->X2, v.c2, 0}, 0,
+        View{-1, 0, 0}, 0, fuse_c2f);
   E.conv("model.3", View{M->X2, v.c2, 0}, 2, View{M->X3, v.c3, 0});
   const int cat14 = v.h12 + v.c3, cat11 = v.c5 + v.c4, cat20 = v.h18 + v.c5,
             cat17 = v.h15 + v.h12;
   E.c2f("model.4", View{M->X3, v.c3, 0}, 3, M->C4, v.c3, v.nm, true,
-        View{M->CAT14, cat14, v.h12});
+        View{M->CAT14, cat14, v.h12}, 0, View{-1, 0, 0}, 0, fuse_c2f);
   E.conv("model.5", View{M->CAT14, cat14, v.h12}, 3, View{M->X5, v.c4, 0});
   E.c2f("model.6", View{M->X5, v.c4, 0}, 4, M->C6, v.c4, v.nm, true,
         View{M->CAT11, cat11, v.c5});
@@ -749,7 +832,7 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
     return r ? r : e;
   };
   E.c2f("model.15", View{M->CAT14, cat14, 0}, 3, M->C15, v.h15, v.nb, false,
-        View{M->X15, v.h15, 0});
+        View{M->X15, v.h15, 0}, 0, View{-1, 0, 0}, 0, fuse_c2f);
   if (E.status || forked_head(0)) return E.status;
   E.conv("model.16", View{M->X15, v.h15, 0}, 3, View{M->CAT17, cat17, 0});
   E.c2f("model.18", View{M->CAT17, cat17, 0}, 4, M->C18, v.h18, v.nb, false,
@@ -928,6 +1011,7 @@ extern "C" int rv_yolo_autotune(void* h, const uint8_t* lb, int B, void* ws, siz
   std::vector<ConvCfg> cands(512);
   for (size_t i = 0; i < L.size() && !st; ++i) {
     const ConvArgs& a = L[i];
+    if (a.fused > 0) continue;  // fused C2f chains have one kernel configuration
     if (verify)
       for (int d = 0; d < 2; ++d)
         if (out_bytes(a, d))

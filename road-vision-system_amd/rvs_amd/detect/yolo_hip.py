@@ -133,6 +133,12 @@ class YoloEngine:
         for h in self._hs:
             call("rv_yolo_set_option", h, 1, 0 if fused else 1)
 
+    def set_fuse_c2f(self, on: bool) -> None:
+        """Narrow C2f blocks as one fused launch (default) or one launch per
+        conv (RV_YOLO_OPT_FUSE_C2F; bit-identical results)."""
+        for h in self._hs:
+            call("rv_yolo_set_option", h, 2, 1 if on else 0)
+
     def letterbox(self, frames: torch.Tensor, slot: int = 0) -> torch.Tensor:
         B = frames.shape[0]
         return kernels.letterbox(frames, self.geo, out=self.lb[slot][:B])

@@ -222,3 +222,42 @@ def test_fused_stem_matches_unfused(cuda):
     assert float((d > ulp_bf16(x1) * 1.01 + 1e-3 * rms).mean()) < 1e-4
     assert (d <= 2 * ulp_bf16(x1) + 1e-2 * rms).all()
     eng.close()
+
+
+@pytest.mark.parametrize("H,W,B,variant", [(1080, 1920, 3, 0), (640, 640, 1, 0), (360, 640, 2, 0)])
+def test_fused_c2f_is_bit_identical(cuda, H, W, B, variant):
+    """The fused C2f chains (c2f.hip: model.2 / model.4 / model.15 bottlenecks
+    + cv2 in one launch each, intermediates in LDS) against one launch per
+    conv, on the production kernel sequence: every output map of the blocks,
+    the raw prediction and the NMS candidates are bit-identical (same MFMA
+    k-order and epilogue)."""
+    from rvs_amd.detect import weights
+    from rvs_amd.detect.yolo_hip import YoloEngine
+    eng = YoloEngine(variant, weights.synthetic_weights(variant, seed=5), B, (H, W), device=cuda)
+    fr = np.stack([cpu.median(cpu.clahe_ycrcb(road_frame(H, W, seed=90 + b)), 3) for b in range(B)])
+    lb = eng.letterbox(torch.from_numpy(fr).to(cuda))
+    eng.set_raw_fused(True)
+    outs = []
+    for fuse in (False, True):
+        eng.set_fuse_c2f(fuse)
+        raw = torch.full((B, 84, eng.A), float("nan"), dtype=torch.float32, device=cuda)
+        eng.forward_raw(lb, raw, slot=int(fuse))
+        torch.cuda.synchronize()
+        ins = Introspect(eng, B)
+        # outputs of the fused blocks: X2 (model.2), the CAT14 slice of model.4,
+        # X15 (model.15) -- located through the trace of the last forward
+        specs, _ = yolo_ref.conv_specs(variant)
+        maps = {}
+        for rec in ins.recs:
+            name, cout = specs[rec[0]][0], specs[rec[0]][2]
+            if name in ("model.2.cv2", "model.4.cv2", "model.15.cv2"):
+                maps[name] = ins.view(rec[8])[..., rec[10]:rec[10] + cout].copy()
+        seg = eng.seg_n[int(fuse)].cpu().numpy().copy()
+        outs.append((raw.cpu().numpy(), maps, seg))
+    (r0, m0, s0), (r1, m1, s1) = outs
+    assert set(m0) == {"model.2.cv2", "model.4.cv2", "model.15.cv2"} == set(m1)
+    for k in m0:
+        np.testing.assert_array_equal(m1[k], m0[k], err_msg=k)
+    np.testing.assert_array_equal(r1, r0)
+    np.testing.assert_array_equal(s1, s0)
+    eng.close()
