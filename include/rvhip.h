@@ -164,6 +164,35 @@ int rv_yolo_destroy(void* handle);
  * 0: one launch per conv. */
 #define RV_YOLO_OPT_FUSE_C2F 2
 int rv_yolo_set_option(void* handle, int opt, int value);
+
+/* fp8 plans (BASELINE configs[4]: "YOLOv8m 1280x1280 fp8 MFMA conv path").
+ * dtype RV_YOLO_DTYPE_FP8: every conv except conv 0 (f32 weights, u8 input)
+ * and the Detect head's last 1x1 stage (bf16, inside the decode) runs on
+ * v_mfma_f32_16x16x32_fp8_fp8 with OCP e4m3fn weights (per output channel
+ * power-of-two scale, round to nearest even, saturated at 448) and e4m3
+ * activations (one power-of-two scale per activation buffer, value = code *
+ * scale, set with rv_yolo_set_act_scales before the first forward; the
+ * head's .1 stage writes bf16 features for the decode).  Packed layout per
+ * fp8 conv: e4m3 [Cout16][ky][kx][Cin64], f32 bias [Cout16], f32 weight
+ * scales [Cout16].  dtype RV_YOLO_DTYPE_BF16 = rv_yolo_pack / rv_yolo_create. */
+#define RV_YOLO_DTYPE_BF16 0
+#define RV_YOLO_DTYPE_FP8 1
+size_t rv_yolo_packed_bytes2(int variant, int dtype);
+int rv_yolo_pack2(int variant, int dtype, const float* flat, size_t n, void* host_out,
+                  size_t out_bytes);
+int rv_yolo_create2(int variant, int dtype, const void* dev_packed, int max_B, int in_h, int in_w,
+                    void** handle);
+/* scales[n]: one per activation buffer (n = rv_yolo_num_buffers; entries of
+ * bf16 / f32 buffers are ignored), each a positive power of two. */
+int rv_yolo_set_act_scales(void* handle, const float* scales, int n);
+/* Per activation buffer: element bytes (1 fp8, 2 bf16, 4 f32), and its name
+ * in the plan ("X0", "C2", "CAT14", "SP", "DA0", "model.2.m.0", ...: the
+ * tensor or concat it holds; the fp8 oracle keys its scales by these). */
+int rv_yolo_buffer_esize(void* handle, int buf);
+int rv_yolo_buffer_name(void* handle, int buf, char* name, int cap);
+/* The power-of-two scale for a tensor of absolute maximum amax (the rule the
+ * packer and calibration use). */
+float rv_fp8_scale(double amax);
 size_t rv_yolo_ws_bytes(void* handle, int B);
 int rv_yolo_num_anchors(void* handle);
 /* Forward on B letterboxed u8 BGR images (B x in_h x in_w x 3).  raw_out

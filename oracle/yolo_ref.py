@@ -90,16 +90,93 @@ def _bf16(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.bfloat16).to(torch.float32)
 
 
+# ---- OCP e4m3fn (the fp8 plan's storage format, include/rvhip.h
+# RV_YOLO_DTYPE_FP8): 4 exponent bits (bias 7), 3 mantissa bits, no
+# infinities, max 448, subnormals in 2^-9 steps.
+def e4m3_table() -> np.ndarray:
+    """Value of every code 0..255 (NaN for 0x7f / 0xff)."""
+    v = np.empty(256, np.float64)
+    for c in range(256):
+        e, m = (c >> 3) & 15, c & 7
+        x = m * 2.0 ** -9 if e == 0 else (1 + m / 8) * 2.0 ** (e - 7)
+        v[c] = -x if c & 128 else x
+    v[0x7F] = v[0xFF] = np.nan
+    return v
+
+
+_E4M3 = e4m3_table()
+_POS = _E4M3[:127]  # codes 0..126: 0 .. 448 ascending
+
+
+def e4m3_code(x: np.ndarray) -> np.ndarray:
+    """Codes of x: saturate to +-448, round to nearest, ties to the even
+    code (v_cvt_pk_fp8_f32's rounding)."""
+    x = np.asarray(x, np.float64)
+    a = np.minimum(np.abs(x), 448.0)
+    hi = np.clip(np.searchsorted(_POS, a, side="left"), 1, 126)
+    lo = hi - 1
+    dl, dh = a - _POS[lo], _POS[hi] - a
+    pick_hi = (dh < dl) | ((dh == dl) & (hi % 2 == 0))
+    c = np.where(pick_hi, hi, lo).astype(np.uint8)
+    c = np.where(a == _POS[hi], hi, c).astype(np.uint8)
+    return np.where(np.signbit(x), c | 0x80, c).astype(np.uint8)
+
+
+def e4m3_value(codes: np.ndarray) -> np.ndarray:
+    return _E4M3[np.asarray(codes, np.uint8)]
+
+
+def fp8_scale(amax: float) -> float:
+    """The power-of-two scale of a tensor with absolute maximum amax
+    (amax / scale in (224, 448]; 1 for amax = 0) -- rv_fp8_scale."""
+    return 1.0 if not amax > 0 else float(2.0 ** math.ceil(math.log2(amax / 448.0)))
+
+
+def quant_fp8(t: torch.Tensor, scale: float) -> torch.Tensor:
+    """Stored value of t in an fp8 buffer of this scale: code(t / s) * s."""
+    q = e4m3_value(e4m3_code(t.detach().double().numpy() / scale)) * scale
+    return torch.from_numpy(q.astype(np.float32))
+
+
+def quant_weight_fp8(w: np.ndarray):
+    """Per output channel power-of-two scale and e4m3 codes of a conv weight
+    [cout][cin][k][k] (rv_yolo_pack2): returns (codes, scales, dequantised)."""
+    w = np.asarray(w, np.float32)
+    amax = np.abs(w.reshape(w.shape[0], -1)).max(1).astype(np.float64)
+    sc = np.array([fp8_scale(a) for a in amax], np.float64)
+    codes = e4m3_code(w / sc.reshape(-1, 1, 1, 1).astype(np.float32))
+    return codes, sc.astype(np.float32), (e4m3_value(codes) * sc.reshape(-1, 1, 1, 1)).astype(np.float32)
+
+
+def _fp8_conv(n: str) -> bool:
+    """Convs the fp8 plan runs in fp8: all but model.0 and the Detect head's
+    last 1x1 stage."""
+    return n != "model.0" and not (n.startswith("model.22.") and n.endswith(".2"))
+
+
 class YoloRef:
     """fp32 CPU forward of YOLOv8 from flat fused weights.
 
     quant=True emulates the HIP path's storage precision (bf16 weights except
     the first conv, bf16 activations rounded once after bias/SiLU/residual,
     f32 head logits) with f32 accumulation, to separate kernel errors from
-    quantisation effects in the parity tests."""
+    quantisation effects in the parity tests.
 
-    def __init__(self, variant: int, flat: np.ndarray, quant: bool = False):
+    quant="fp8" emulates the fp8 plan (RV_YOLO_DTYPE_FP8): e4m3 weights with
+    per-cout power-of-two scales (quant_weight_fp8), every activation stored
+    as e4m3 codes of its BUFFER's scale (`scales`: plan buffer name -> scale,
+    EngineYolo.buffers() names; a tensor written to two buffers is rounded
+    once per buffer), the head's .1 features in bf16, its .2 stage bf16
+    weights and f32 logits."""
+
+    def __init__(self, variant: int, flat: np.ndarray, quant=False, scales=None):
         self.quant = quant
+        # scales="record": the fp8 graph with fp8 weights but unrounded
+        # activations, recording each buffer's amax (fp8_calibration)
+        self.amax = {} if scales == "record" else None
+        self.scales = {} if scales == "record" else dict(scales or {})
+        if quant == "fp8" and not self.scales and self.amax is None:
+            raise ValueError("quant='fp8' needs the per-buffer activation scales")
         self.specs, meta = conv_specs(variant)
         self.nb, self.nm = meta["nb"], meta["nm"]
         self.p = {}
@@ -110,7 +187,9 @@ class YoloRef:
             w = torch.from_numpy(flat[off:off + nw].reshape(co, ci, k, k).copy())
             b = torch.from_numpy(flat[off + nw:off + nw + co].copy())
             off += nw + co
-            if quant and n != "model.0":
+            if quant == "fp8" and _fp8_conv(n):
+                w = torch.from_numpy(quant_weight_fp8(w.numpy())[2])
+            elif quant and n != "model.0":
                 w = _bf16(w)
             self.p[n] = (w, b, s, k, act)
         assert off == flat.size, "flat weight size mismatch"
@@ -147,9 +226,33 @@ class YoloRef:
         y = F.silu(y) if act else y
         if res is not None:
             y = res + y
+        if self.quant == "fp8":
+            if n.startswith("model.22.") and n.endswith(".1"):
+                y = _bf16(y)  # the decode's bf16 features
+            return y  # fp8 rounding happens per destination buffer (Q)
         if self.quant and not (n.startswith("model.22.") and n.endswith(".2")):
             y = _bf16(y)
         return y
+
+    def Q(self, t: torch.Tensor, buf: str) -> torch.Tensor:
+        """t as stored in plan buffer `buf` (fp8 mode; identity otherwise)."""
+        if self.quant != "fp8":
+            return t
+        if self.amax is not None:
+            self.amax[buf] = max(self.amax.get(buf, 0.0), float(t.abs().max()))
+            return t
+        return quant_fp8(t, self.scales[buf])
+
+    def c2f8(self, p, x, n, shortcut, cb):
+        """C2f of the fp8 plan: cv1 and the bottleneck outputs in concat
+        buffer cb, bottleneck temps in "<p>.m.<i>"; returns cv2's unrounded
+        output."""
+        y = list(self.Q(self.conv(p + ".cv1", x), cb).chunk(2, 1))
+        for i in range(n):
+            t = y[-1]
+            m = self.Q(self.conv(f"{p}.m.{i}.cv1", t), f"{p}.m.{i}")
+            y.append(self.Q(self.conv(f"{p}.m.{i}.cv2", m, res=t if shortcut else None), cb))
+        return self.conv(p + ".cv2", torch.cat(y, 1))
 
     def c2f(self, p, x, n, shortcut):
         y = list(self.conv(p + ".cv1", x).chunk(2, 1))
@@ -167,8 +270,47 @@ class YoloRef:
         return self.conv("model.9.cv2", torch.cat([x, y1, y2, y3], 1))
 
     @torch.no_grad()
+    def _backbone_fp8(self, x: torch.Tensor):
+        """The fp8 plan's graph, buffer by buffer (csrc/yolo.hip plan() /
+        rv_yolo_forward)."""
+        Q, up = self.Q, (lambda t: F.interpolate(t, scale_factor=2, mode="nearest"))  # noqa: E731
+        x = Q(self.conv("model.0", x), "X0")
+        x = Q(self.conv("model.1", x), "X1")
+        x = Q(self.c2f8("model.2", x, self.nb, True, "C2"), "X2")
+        x = Q(self.conv("model.3", x), "X3")
+        p4 = Q(self.c2f8("model.4", x, self.nm, True, "C4"), "CAT14")
+        x = Q(self.conv("model.5", p4), "X5")
+        p6 = Q(self.c2f8("model.6", x, self.nm, True, "C6"), "CAT11")
+        x = Q(self.conv("model.7", p6), "X7")
+        x = Q(self.c2f8("model.8", x, self.nb, True, "C8"), "X8")
+        s = Q(self.conv("model.9.cv1", x), "SP")
+        y1 = F.max_pool2d(s, 5, 1, 2)
+        y2 = F.max_pool2d(y1, 5, 1, 2)
+        y3 = F.max_pool2d(y2, 5, 1, 2)
+        p9 = self.conv("model.9.cv2", torch.cat([s, y1, y2, y3], 1))
+        p9_20, p9_11 = Q(p9, "CAT20"), Q(p9, "CAT11")
+        p12 = self.c2f8("model.12", torch.cat([up(p9_11), p6], 1), self.nb, False, "C12")
+        p12_17, p12_14 = Q(p12, "CAT17"), Q(p12, "CAT14")
+        p15 = Q(self.c2f8("model.15", torch.cat([up(p12_14), p4], 1), self.nb, False, "C15"), "X15")
+        x16 = Q(self.conv("model.16", p15), "CAT17")
+        p18 = Q(self.c2f8("model.18", torch.cat([x16, p12_17], 1), self.nb, False, "C18"), "X18")
+        x19 = Q(self.conv("model.19", p18), "CAT20")
+        p21 = Q(self.c2f8("model.21", torch.cat([x19, p9_20], 1), self.nb, False, "C21"), "X21")
+        outs = []
+        for i, f in enumerate((p15, p18, p21)):
+            c = lambda n, t: self.conv(f"model.22.{n}", t)  # noqa: E731
+            da_b = Q(c(f"cv2.{i}.0", f), f"DA{i}")
+            da_c = Q(c(f"cv3.{i}.0", f), f"DA{i}")
+            box = c(f"cv2.{i}.2", c(f"cv2.{i}.1", da_b))
+            cls = c(f"cv3.{i}.2", c(f"cv3.{i}.1", da_c))
+            outs.append(torch.cat([box, cls], 1))
+        return outs
+
+    @torch.no_grad()
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """x: (B,3,H,W) f32 RGB in [0,1] -> raw (B, 84, A)."""
+        if self.quant == "fp8":
+            return self._decode(self._backbone_fp8(x))
         up = lambda t: F.interpolate(t, scale_factor=2, mode="nearest")  # noqa: E731
         x = self.conv("model.0", x)
         x = self.conv("model.1", x)
@@ -184,15 +326,22 @@ class YoloRef:
         p15 = self.c2f("model.15", torch.cat([up(p12), p4], 1), self.nb, False)
         p18 = self.c2f("model.18", torch.cat([self.conv("model.16", p15), p12], 1), self.nb, False)
         p21 = self.c2f("model.21", torch.cat([self.conv("model.19", p18), p9], 1), self.nb, False)
-        feats = [p15, p18, p21]
-        outs, anchors, strides = [], [], []
-        for i, f in enumerate(feats):
+        outs = []
+        for i, f in enumerate((p15, p18, p21)):
             box = self.conv(f"model.22.cv2.{i}.2", self.conv(f"model.22.cv2.{i}.1",
                                                              self.conv(f"model.22.cv2.{i}.0", f)))
             cls = self.conv(f"model.22.cv3.{i}.2", self.conv(f"model.22.cv3.{i}.1",
                                                              self.conv(f"model.22.cv3.{i}.0", f)))
-            outs.append(torch.cat([box, cls], 1).flatten(2))
-            h, w = f.shape[2:]
+            outs.append(torch.cat([box, cls], 1))
+        return self._decode(outs)
+
+    @staticmethod
+    def _decode(levels):
+        """Detect's inference tail on the per-level (B, 144, h, w) logits."""
+        outs, anchors, strides = [], [], []
+        for i, lv in enumerate(levels):
+            outs.append(lv.flatten(2))
+            h, w = lv.shape[2:]
             s = 8 * 2 ** i
             sy, sx = torch.meshgrid(torch.arange(h, dtype=torch.float32) + 0.5,
                                     torch.arange(w, dtype=torch.float32) + 0.5, indexing="ij")
@@ -211,6 +360,14 @@ class YoloRef:
         x2y2 = anc + rb
         dbox = torch.cat([(x1y1 + x2y2) / 2, x2y2 - x1y1], 1) * st
         return torch.cat([dbox, cls.sigmoid()], 1)
+
+
+def fp8_calibration(variant: int, flat: np.ndarray, x: torch.Tensor) -> dict:
+    """Buffer name -> fp8_scale(amax) over the fp8 graph on x (the oracle's
+    own calibration; the HIP engine calibrates on its bf16 plan)."""
+    m = YoloRef(variant, flat, quant="fp8", scales="record")
+    m.forward(x)
+    return {k: fp8_scale(v) for k, v in m.amax.items()}
 
 
 def preprocess(lb_bgr: np.ndarray) -> torch.Tensor:

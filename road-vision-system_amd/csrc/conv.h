@@ -41,6 +41,15 @@ struct ConvArgs {
   // > 0: this launch record stands for a fused C2f chain (yolo.hip's
   // Model::fused[fused - 1]); the autotuner leaves it alone
   int fused;
+  // fp8 (OCP e4m3fn) path: in8 = 1 -> the input (and residual) views hold
+  // fp8 codes with per-tensor scales s_in / s_res (value = code * s), the
+  // weights are fp8 [Cout_pad16][ky][kx][Cin_pad64] with per-cout scales
+  // `wscale` (g2: g2_wscale); out*_8 = 1 -> that output view stores fp8
+  // codes of value / s_out*, else bf16 (f32 when out_f32).
+  int in8, out0_8, out1_8;
+  float s_in, s_res, s_out0, s_out1;
+  const float* wscale;
+  const float* g2_wscale;
 };
 
 // One configuration of the LDS-staged conv kernel: MR x NR 16x16 fragments
@@ -65,6 +74,10 @@ int conv_candidates(const ConvArgs& a, ConvCfg* out, int cap);
 // (predictor preprocess: im[..., ::-1] / 255).  w: [C0][3 rgb][3][3] f32.
 int launch_conv0(const uint8_t* img, int B, int H, int W, const float* w, const float* bias,
                  int C0, bf16_t* out, int out_cs, hipStream_t s);
+// The same with an fp8 output (codes of value / s_out, channel stride out_cs
+// bytes).
+int launch_conv0_fp8(const uint8_t* img, int B, int H, int W, const float* w, const float* bias,
+                     int C0, uint8_t* out, int out_cs, float s_out, hipStream_t s);
 
 // conv0 and model.1 (C0 = 16 -> C1 = 32, k3 s2) fused: the P1 map never
 // leaves LDS.  w1/b1: model.1's packed weights / bias; out: X1 (NHWC,
@@ -76,6 +89,8 @@ int launch_stem(const uint8_t* img, int B, int H, int W, const float* w0, const 
 // SPPF pooling: buf holds x in channels [0, c); writes maxpool5, maxpool5^2
 // and maxpool5^3 (= clipped 5/9/13 windows) into [c,2c), [2c,3c), [3c,4c).
 int launch_sppf_pool(bf16_t* buf, int B, int H, int W, int c, hipStream_t s);
+// fp8 buffer (one scale for the whole buffer: max pooling is scale-free).
+int launch_sppf_pool_fp8(uint8_t* buf, int B, int H, int W, int c, hipStream_t s);
 
 // Fused C2f bottleneck chain + cv2 (c2f.hip) for C2f blocks with hidden
 // width C in {16, 32} and N in {1, 2} bottlenecks (C = 16: N = 1): reads

@@ -221,6 +221,11 @@ static int try_launch_patch(const ConvArgs& a, hipStream_t s, int* st);
 int launch_conv(const ConvArgs& a, hipStream_t s) {
   int st = 0;
   if (try_launch_patch(a, s, &st)) return st;
+  if (a.in8) {
+    set_error("fp8 conv (Cin %d, Cout %d, k%d s%d) has no patch-kernel configuration", a.Cin,
+              a.Cout, a.k, a.stride);
+    return RV_EINVAL;
+  }
   if (a.g2_cout0 > 0) {
     set_error("grouped conv (Cout %d, split %d) has no patch-kernel configuration", a.Cout,
               a.g2_cout0);
@@ -391,6 +396,74 @@ constexpr int patch_maxit() {
   return (S == 2 ? 6 : 2) * NR + 2;
 }
 
+// fp8 epilogue (ConvArgs::in8): dequantise (acc * wscale[co] * s_in), bias,
+// SiLU, residual (fp8 code * s_res), then per output view fp8 codes of
+// value / s_out (v_cvt_pk_fp8_f32, round to nearest even, saturated to
+// +-448 first) or bf16 / f32.
+__device__ __forceinline__ uint32_t f8_encode4(const float (&v)[4], float inv_s) {
+  float q[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = fminf(fmaxf(v[i] * inv_s, -448.f), 448.f);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], w, true);
+  return (uint32_t)w;
+}
+
+template <int MR, int NR>
+__device__ __forceinline__ void epilogue8(const ConvArgs& a, f32x4 (&acc)[MR][NR], int cout0,
+                                          const bool (&pv)[NR], const int (&pb)[NR],
+                                          const int (&py)[NR], const int (&px)[NR], int quad,
+                                          const f32x4 (&bias)[MR], const f32x4 (&dq)[MR]) {
+  const float inv0 = 1.0f / a.s_out0, inv1 = 1.0f / a.s_out1;
+#pragma unroll
+  for (int n = 0; n < NR; ++n) {
+    if (!pv[n]) continue;
+    const int b = pb[n], oy = py[n], ox = px[n];
+    const size_t opix = ((size_t)b * a.Ho + oy) * a.Wo + ox;
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      const int co = cout0 + m * 16 + quad * 4;
+      if (co >= a.Cout) continue;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[m][n][i] * dq[m][i] + bias[m][i];
+      if (a.act) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = silu(v[i]);
+      }
+      if (a.res) {
+        const uint32_t rr = *(const uint32_t*)((const uint8_t*)a.res + opix * a.res_cs + a.res_co + co);
+        v[0] += __builtin_amdgcn_cvt_f32_fp8((int)rr, 0) * a.s_res;
+        v[1] += __builtin_amdgcn_cvt_f32_fp8((int)rr, 1) * a.s_res;
+        v[2] += __builtin_amdgcn_cvt_f32_fp8((int)rr, 2) * a.s_res;
+        v[3] += __builtin_amdgcn_cvt_f32_fp8((int)rr, 3) * a.s_res;
+      }
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        void* outp = d == 0 ? a.out0 : a.out1;
+        if (!outp) continue;
+        const int cs_ = d == 0 ? a.out0_cs : a.out1_cs;
+        const int co_ = (d == 0 ? a.out0_co : a.out1_co) + co;
+        const int up = d == 0 ? a.out0_up : a.out1_up;
+        const int o8 = d == 0 ? a.out0_8 : a.out1_8;
+        const int ny = up ? 2 : 1;
+        for (int dy = 0; dy < ny; ++dy)
+          for (int dx = 0; dx < ny; ++dx) {
+            const size_t q = up ? ((size_t)(b * 2 * a.Ho + 2 * oy + dy) * (2 * a.Wo) + 2 * ox + dx) : opix;
+            if (o8) {
+              *(uint32_t*)((uint8_t*)outp + q * cs_ + co_) = f8_encode4(v, d == 0 ? inv0 : inv1);
+            } else if (a.out_f32) {
+              *(float4*)((float*)outp + q * cs_ + co_) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+              *(uint2*)((uint16_t*)outp + q * cs_ + co_) =
+                  make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+            }
+          }
+      }
+    }
+  }
+}
+
 // Persistent, software-pipelined form: the block owns cout tile blockIdx.y
 // and walks pixel tiles blockIdx.x, +gridDim.x, ...  A step is (tile, group
 // of G input-channel chunks); the DMA of step s+1 -- the next group or the
@@ -406,7 +479,12 @@ constexpr int patch_maxit() {
 // own input channel slice / weights / bias (a block-diagonal conv: the
 // Detect head's cv2 and cv3 branches in one launch).  The host keeps every
 // tile inside one group.
-template <int MR, int NR, int K, int S, bool RESW>
+// F8 = true: fp8 e4m3 inputs / weights (ConvArgs::in8).  A pipeline chunk
+// is 64 channels (64 B per pixel slot, the same LDS image as the bf16
+// kernel's 32-channel chunk); each tap runs two v_mfma_f32_16x16x32_fp8_fp8
+// per chunk (channels 0-31 and 32-63), each lane reading 8 of its 16-B
+// quarter pair (logical quarter 2h + quad/2, byte (quad & 1) * 8).
+template <int MR, int NR, int K, int S, bool RESW, bool F8>
 __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int T2 = K * K;
@@ -416,6 +494,8 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
   static_assert(MAXP <= 32, "tail mask is 32 bits");
   constexpr int WJ = BC * T2 / 16;            // weight DMA instructions per chunk
   constexpr int MAXW = (WJ + 3) / 4;
+  constexpr int EB = F8 ? 1 : 2;              // bytes per element
+  constexpr int CC = F8 ? 64 : 32;            // channels per chunk (64 B per pixel)
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int col = lane & 15, quad = lane >> 4;
@@ -423,20 +503,22 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
   // the tile's group: its input slice, weights, bias and weight row base wc0
   int wc0 = cout0, gcout = a.g2_cout0 > 0 ? a.g2_cout0 : a.Cout;
   int in_co = a.in_co, Cin = a.Cin;
-  const bf16_t* wts = a.w;
+  const uint8_t* wts = (const uint8_t*)a.w;
   const float* bias_p = a.bias;
+  const float* wsc_p = a.wscale;
   if (a.g2_cout0 > 0 && cout0 >= a.g2_cout0) {
     wc0 = cout0 - a.g2_cout0;
     gcout = a.Cout - a.g2_cout0;
     in_co = a.g2_in_co;
     Cin = a.g2_Cin;
-    wts = a.g2_w;
+    wts = (const uint8_t*)a.g2_w;
     bias_p = a.g2_bias;
+    wsc_p = a.g2_wscale;
   }
   const int wcout_pad = (gcout + 15) & ~15;
-  const int cin_pad = (Cin + 31) & ~31;
-  const int Kp = T2 * cin_pad;
-  const int nch = cin_pad >> 5;
+  const int cin_pad = (Cin + CC - 1) & ~(CC - 1);
+  const int Kp = T2 * cin_pad;                // weight row length (elements)
+  const int nch = cin_pad / CC;
   const int G = g.G < nch ? g.G : nch;
   const int ngrp = (nch + G - 1) / G;
   const int chunk_bytes = g.p_bytes + (RESW ? 0 : W_BYTES);
@@ -452,6 +534,8 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
 
   // block-constant: output slots -> (r, cc) of the tile, patch byte base
   constexpr int PB = patch_pixb<S>(), SL = PB / 16;
+  // fp8: lane quad reads channel half 0 at logical quarter quad / 2; half 1
+  // (quarter + 2) is the same address XOR 32 (the swizzle XORs the quarter)
   int orow[NR], ocol[NR], boff[NR][K];
   bool oin[NR];
 #pragma unroll
@@ -465,24 +549,29 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
 #pragma unroll
     for (int kx = 0; kx < K; ++kx) {
       const int sc = patch_scol<S>(pc + kx, g.PW);
-      boff[n][kx] = (pr * g.PW + sc) * 64 + ((quad ^ ((sc >> 2) & 3)) << 4);
+      const int lq = F8 ? quad >> 1 : quad;
+      boff[n][kx] = (pr * g.PW + sc) * 64 + ((lq ^ ((sc >> 2) & 3)) << 4) + (F8 ? (quad & 1) * 8 : 0);
     }
   }
-  f32x4 bias[MR];
+  f32x4 bias[MR], dq[MR];
 #pragma unroll
   for (int m = 0; m < MR; ++m) {
     const int co = wc0 + m * 16 + quad * 4;  // bias is padded to Cout_pad16
     bias[m] = co < wcout_pad ? *(const f32x4*)(bias_p + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (F8) {
+      const f32x4 ws = co < wcout_pad ? *(const f32x4*)(wsc_p + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+      dq[m] = ws * a.s_in;
+    }
   }
   int poff[MAXP];
   uint32_t tailbad = 0;  // bit it: this lane's quarter is >= Cin in the last chunk
-  const bf16_t* img = a.in;
+  const uint8_t* img = (const uint8_t*)a.in;
   auto prep_tile = [&](int ti) {
     const int b = ti / tiles_img;
     const int r = ti - b * tiles_img;
     const int ty = r / g.tiles_x, tx = r - (r / g.tiles_x) * g.tiles_x;
     const int iy0 = ty * g.R * S - pad, ix0 = tx * g.C * S - pad;
-    img = a.in + (size_t)b * a.Hin * a.Win * a.in_cs + in_co;
+    img = (const uint8_t*)a.in + ((size_t)b * a.Hin * a.Win * a.in_cs + in_co) * EB;
     tailbad = 0;
 #pragma unroll
     for (int it = 0; it < MAXP; ++it) {
@@ -496,13 +585,13 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
       const int sq = q ^ ((sc >> 2) & 3);  // source quarter of slot q
       const bool ok = pix < npp && (unsigned)iy < (unsigned)a.Hin &&
                       (unsigned)ix < (unsigned)a.Win;
-      poff[it] = ok ? (iy * a.Win + ix) * a.in_cs + sq * 8 : -1;
-      if ((nch - 1) * 32 + sq * 8 >= Cin) tailbad |= 1u << it;
+      poff[it] = ok ? (iy * a.Win + ix) * a.in_cs * EB + sq * 16 : -1;
+      if ((nch - 1) * CC + sq * (16 / EB) >= Cin) tailbad |= 1u << it;
     }
   };
   // weight DMA: instruction j moves (row, tap) pairs 16 j .. 16 j + 15, a
-  // quarter (8 channels of chunk c) per lane; offsets are recomputed per
-  // call (constant divisor, no registers held across the loop)
+  // 16-B quarter of chunk c per lane; offsets are recomputed per call
+  // (constant divisor, no registers held across the loop)
   auto dma_weights = [&](int c, uint8_t* Wl) {
 #pragma unroll
     for (int it = 0; it < MAXW; ++it) {
@@ -512,8 +601,9 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
         const int row = pr / T2, tap = pr - (pr / T2) * T2;
         const int q = (lane & 3) ^ swz(row);
         const int co = wc0 + row;
-        const void* src = co < wcout_pad ? (const void*)(wts + co * Kp + tap * cin_pad + q * 8 + c * 32)
-                                         : (const void*)g_zero16;
+        const void* src = co < wcout_pad
+                              ? (const void*)(wts + ((size_t)co * Kp + tap * cin_pad) * EB + q * 16 + c * 64)
+                              : (const void*)g_zero16;
         __builtin_amdgcn_global_load_lds(src, (void*)(Wl + j * 1024), 16, 0, 0);
       }
     }
@@ -529,7 +619,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
         const int j = wave + 4 * it;
         if (j < g.pinst) {
           const void* src = (poff[it] >= 0 && !((bad >> it) & 1))
-                                ? (const void*)(img + poff[it] + c * 32)
+                                ? (const void*)(img + poff[it] + c * 64)
                                 : (const void*)g_zero16;
           __builtin_amdgcn_global_load_lds(src, (void*)(P + j * 1024), 16, 0, 0);
         }
@@ -546,27 +636,48 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
       const uint8_t* Wl = RESW ? smem + c * W_BYTES : P + g.p_bytes;
       // kernel rows are not unrolled for the largest tiles: the fragments of
       // one row (3 taps) in flight keep them under the register file
-#pragma unroll(MR * NR >= 16 ? 1 : K)
+#pragma unroll(F8 || MR * NR >= 16 ? 1 : K)
       for (int ky = 0; ky < K; ++ky) {
         const uint8_t* Prow = P + ky * g.PW * PB;
 #pragma unroll
         for (int kx = 0; kx < K; ++kx) {
           const int tap = ky * K + kx;
-          bf16x8 A[MR], Bf[NR];
+          if constexpr (F8) {
 #pragma unroll
-          for (int m = 0; m < MR; ++m) {
-            const int row = m * 16 + col;
-            A[m] = __builtin_bit_cast(
-                bf16x8, *(const uint4*)(Wl + (row * T2 + tap) * 64 + ((quad ^ swz(row)) << 4)));
-          }
+            for (int hh = 0; hh < 2; ++hh) {
+              long A[MR], Bf[NR];
 #pragma unroll
-          for (int n = 0; n < NR; ++n)
-            Bf[n] = __builtin_bit_cast(bf16x8, *(const uint4*)(Prow + boff[n][kx]));
+              for (int m = 0; m < MR; ++m) {
+                const int row = m * 16 + col;
+                A[m] = *(const long*)(Wl + (((row * T2 + tap) * 64 +
+                                             (((quad >> 1) ^ swz(row)) << 4) + (quad & 1) * 8) ^
+                                            (hh << 5)));
+              }
 #pragma unroll
-          for (int m = 0; m < MR; ++m)
+              for (int n = 0; n < NR; ++n) Bf[n] = *(const long*)(Prow + (boff[n][kx] ^ (hh << 5)));
+#pragma unroll
+              for (int m = 0; m < MR; ++m)
+#pragma unroll
+                for (int n = 0; n < NR; ++n)
+                  acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(A[m], Bf[n], acc[m][n], 0, 0, 0);
+            }
+          } else {
+            bf16x8 A[MR], Bf[NR];
+#pragma unroll
+            for (int m = 0; m < MR; ++m) {
+              const int row = m * 16 + col;
+              A[m] = __builtin_bit_cast(
+                  bf16x8, *(const uint4*)(Wl + (row * T2 + tap) * 64 + ((quad ^ swz(row)) << 4)));
+            }
 #pragma unroll
             for (int n = 0; n < NR; ++n)
-              acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[m], Bf[n], acc[m][n], 0, 0, 0);
+              Bf[n] = __builtin_bit_cast(bf16x8, *(const uint4*)(Prow + boff[n][kx]));
+#pragma unroll
+            for (int m = 0; m < MR; ++m)
+#pragma unroll
+              for (int n = 0; n < NR; ++n)
+                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[m], Bf[n], acc[m][n], 0, 0, 0);
+          }
         }
       }
     }
@@ -607,7 +718,10 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
         px[n] = tx * g.C + ocol[n];
         pv[n] = oin[n] && py[n] < a.Ho && px[n] < a.Wo;
       }
-      epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias);
+      if constexpr (F8)
+        epilogue8<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias, dq);
+      else
+        epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias);
       ti += gridDim.x;
       grp = 0;
     } else {
@@ -739,7 +853,8 @@ __global__ __launch_bounds__(256, 2) void conv1x1_direct_kernel(ConvArgs a) {
 static int conv_nch(const ConvArgs& a) {
   int cin = a.Cin;
   if (a.g2_cout0 > 0 && a.g2_Cin > cin) cin = a.g2_Cin;
-  return (cin + 31) / 32;
+  const int cc = a.in8 ? 64 : 32;  // channels per chunk (64 B per pixel either way)
+  return (cin + cc - 1) / cc;
 }
 
 static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& smem) {
@@ -796,11 +911,11 @@ static int num_cus() {
 
 // Every instantiation gets the full 160 KB dynamic-LDS cap once; resident
 // blocks per CU are cached per LDS size (per instantiation).
-template <int MR, int NR, int K, int S, bool RESW>
+template <int MR, int NR, int K, int S, bool RESW, bool F8 = false>
 static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, int persist,
                           hipStream_t s) {
   static bool attr = false;
-  auto fn = conv_patch_kernel<MR, NR, K, S, RESW>;
+  auto fn = conv_patch_kernel<MR, NR, K, S, RESW, F8>;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        160 * 1024);
@@ -901,9 +1016,35 @@ constexpr bool patch_spills(int MR, int NR, int K, int S, bool RESW) {
   return !RESW && K == 3 && ((S == 1 && MR * NR > 16) || (S == 2 && MR * NR >= 8));
 }
 
+// fp8 instantiations: MR, NR in {1, 2, 4}; the 3x3 ones that exceed the
+// register file (4x4, and 1x2 stride 2 with staged weights) are not built
+template <int MR, int NR>
+constexpr bool tile8_built() {
+  return (MR == 1 || MR == 2 || MR == 4) && (NR == 1 || NR == 2 || NR == 4);
+}
+constexpr bool patch_spills8(int MR, int NR, int K, int S, bool RESW) {
+  return K == 3 && (MR * NR >= 16 || (S == 2 && !RESW && MR == 1 && NR == 2));
+}
+
 template <int MR, int NR, bool RESW>
 static int launch_patch_ks(const ConvArgs& a, const PatchGeo& g, size_t smem, int persist,
                            hipStream_t s) {
+  if (a.in8) {
+    if constexpr (tile8_built<MR, NR>()) {
+      if constexpr (!patch_spills(MR, NR, 3, 1, RESW) && !patch_spills8(MR, NR, 3, 1, RESW))
+        if (a.k == 3 && a.stride == 1)
+          return launch_patch_t<MR, NR, 3, 1, RESW, true>(a, g, smem, persist, s);
+      if (a.k == 1 && a.stride == 1)
+        return launch_patch_t<MR, NR, 1, 1, RESW, true>(a, g, smem, persist, s);
+      if constexpr (patch_s2_ok<MR, NR>() && !patch_spills(MR, NR, 3, 2, RESW) &&
+                    !patch_spills8(MR, NR, 3, 2, RESW)) {
+        if (a.k == 3 && a.stride == 2)
+          return launch_patch_t<MR, NR, 3, 2, RESW, true>(a, g, smem, persist, s);
+      }
+    }
+    set_error("conv_patch (fp8): no variant MR=%d NR=%d k=%d s=%d", MR, NR, a.k, a.stride);
+    return RV_EINVAL;
+  }
   if constexpr (!patch_spills(MR, NR, 3, 1, RESW))
     if (a.k == 3 && a.stride == 1) return launch_patch_t<MR, NR, 3, 1, RESW>(a, g, smem, persist, s);
   if (a.k == 1 && a.stride == 1) return launch_patch_t<MR, NR, 1, 1, RESW>(a, g, smem, persist, s);
@@ -919,13 +1060,19 @@ static const int kTiles[][2] = {{8, 2}, {8, 1}, {5, 2}, {5, 1}, {4, 4}, {4, 2}, 
                                 {2, 4}, {2, 2}, {2, 1}, {1, 4}, {1, 2}, {1, 1}};
 
 bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c) {
-  if (c.kind == 1) return direct_ok(a, c);
+  if (c.kind == 1) return !a.in8 && direct_ok(a, c);
   if (c.kind != 0) return false;
+  if (a.in8 && !((c.mr == 1 || c.mr == 2 || c.mr == 4) && (c.nr == 1 || c.nr == 2 || c.nr == 4)))
+    return false;
+  if (a.in8 && (a.Cin % 16 || a.in_co % 16 || a.in_cs % 16 ||
+                 (a.g2_cout0 > 0 && (a.g2_Cin % 16 || a.g2_in_co % 16))))
+    return false;  // whole 16-B quarters of fp8 channels
   const int T = (a.Cout + 15) / 16;
   if (c.mr > T && c.mr > 1) return false;
   if (a.stride == 2 && (c.nr > 2 || c.mr * c.nr > 8 || a.k != 3)) return false;  // patch_s2_ok
   if (a.g2_cout0 > 0 && a.g2_cout0 % (16 * c.mr) != 0) return false;  // tiles inside one group
   if (patch_spills(c.mr, c.nr, a.k, a.stride, c.resw != 0)) return false;
+  if (a.in8 && patch_spills8(c.mr, c.nr, a.k, a.stride, c.resw != 0)) return false;
   PatchGeo g;
   size_t sm;
   return patch_geo(a, c, g, sm);
@@ -978,7 +1125,7 @@ int conv_candidates(const ConvArgs& a, ConvCfg* out, int cap) {
     // 1x1 layers: the direct-B kernel
     for (int persist = 1; persist >= 0; --persist) {
       const ConvCfg d{t[0], t[1], 1, 1, persist, 1};
-      if (direct_ok(a, d)) {
+      if (!a.in8 && direct_ok(a, d)) {
         if (n < cap) out[n] = d;
         ++n;
       }
@@ -1068,11 +1215,12 @@ constexpr int kC0TH = 8, kC0TW = 64;
 constexpr int kC0IW = (2 * kC0TW + 1) * 3;  // 387 bytes per input row
 constexpr int kC0RS = kC0IW + 5;            // LDS row stride (u16 elements, 8-B multiple)
 
-template <int MR>
+template <int MR, bool F8 = false>
 __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ img, int B, int H,
                                                     int W, const float* __restrict__ w,
                                                     const float* __restrict__ bias,
-                                                    uint16_t* __restrict__ out, int out_cs) {
+                                                    void* __restrict__ out, int out_cs,
+                                                    float s_out = 1.f) {
   __shared__ uint16_t xin[(2 * kC0TH + 1) * kC0RS];
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
   const int tiles_x = (Wo + kC0TW - 1) / kC0TW;
@@ -1181,12 +1329,18 @@ __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ 
     }
     const int ox = ox0 + 16 * wave + col;
     if (oy < Ho && ox < Wo) {
-      uint16_t* o = out + (((size_t)b * Ho + oy) * Wo + ox) * out_cs;
+      const size_t opix = (((size_t)b * Ho + oy) * Wo + ox) * out_cs;
 #pragma unroll
       for (int m = 0; m < MR; ++m) {
         const float v0 = silu(acc[m][0] + bv[m][0]), v1 = silu(acc[m][1] + bv[m][1]);
         const float v2 = silu(acc[m][2] + bv[m][2]), v3 = silu(acc[m][3] + bv[m][3]);
-        *(uint2*)(o + 16 * m + 4 * quad) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+        if constexpr (F8) {
+          const float v[4] = {v0, v1, v2, v3};
+          *(uint32_t*)((uint8_t*)out + opix + 16 * m + 4 * quad) = f8_encode4(v, 1.0f / s_out);
+        } else {
+          *(uint2*)((uint16_t*)out + opix + 16 * m + 4 * quad) =
+              make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+        }
       }
     }
   }
@@ -1206,6 +1360,22 @@ int launch_conv0(const uint8_t* img, int B, int H, int W, const float* w, const 
     return RV_EINVAL;
   }
   return launch_status("conv0");
+}
+
+int launch_conv0_fp8(const uint8_t* img, int B, int H, int W, const float* w, const float* bias,
+                     int C0, uint8_t* out, int out_cs, float s_out, hipStream_t s) {
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  const int blocks = B * ceil_div(Ho, kC0TH) * ceil_div(Wo, kC0TW);
+  if (C0 == 16) conv0_kernel<1, true><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs, s_out);
+  else if (C0 == 32) conv0_kernel<2, true><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs, s_out);
+  else if (C0 == 48) conv0_kernel<3, true><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs, s_out);
+  else if (C0 == 64) conv0_kernel<4, true><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs, s_out);
+  else if (C0 == 80) conv0_kernel<5, true><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs, s_out);
+  else {
+    set_error("conv0 C0=%d unsupported", C0);
+    return RV_EINVAL;
+  }
+  return launch_status("conv0_fp8");
 }
 
 // ---------------------------------------------------------------------------
@@ -1458,91 +1628,138 @@ __device__ __forceinline__ uint4 f_to_bf8(const float (&f)[8]) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-__global__ __launch_bounds__(256) void sppf_pool_kernel(uint16_t* __restrict__ buf, int B, int H,
+// 16-B vector <-> its lanes as f32: 8 bf16 values, or 16 fp8 codes (one
+// buffer scale, so the max over codes' values re-encodes exactly).
+template <bool F8>
+struct SppfVec {
+  static constexpr int N = F8 ? 16 : 8;
+  __device__ static void dec(const uint4 v, float (&f)[N]) {
+    if constexpr (F8) {
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[4 * j] = __builtin_amdgcn_cvt_f32_fp8((int)w[j], 0);
+        f[4 * j + 1] = __builtin_amdgcn_cvt_f32_fp8((int)w[j], 1);
+        f[4 * j + 2] = __builtin_amdgcn_cvt_f32_fp8((int)w[j], 2);
+        f[4 * j + 3] = __builtin_amdgcn_cvt_f32_fp8((int)w[j], 3);
+      }
+    } else {
+      bf8_to_f(v, f);
+    }
+  }
+  __device__ static uint4 enc(const float (&f)[N]) {
+    if constexpr (F8) {
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float q[4] = {f[4 * j], f[4 * j + 1], f[4 * j + 2], f[4 * j + 3]};
+        w[j] = f8_encode4(q, 1.f);
+      }
+      return make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      return f_to_bf8(f);
+    }
+  }
+};
+
+template <bool F8>
+__global__ __launch_bounds__(256) void sppf_pool_kernel(uint8_t* __restrict__ buf, int B, int H,
                                                         int W, int c) {
+  using V = SppfVec<F8>;
+  constexpr int NV = V::N, EB = F8 ? 1 : 2;
   extern __shared__ __attribute__((aligned(16))) uint4 sp[];  // x, h5, h9, h13: [H*W] uint4 each
-  const int groups = c / 8;
+  const int groups = c / NV;
   const int b = blockIdx.x / groups, g = blockIdx.x - (blockIdx.x / groups) * groups;
-  const int cs = 4 * c;
+  const int cs = 4 * c * EB;  // pixel stride, bytes
   const int HW = H * W;
   uint4* xs = sp;
   uint4* h5 = sp + HW;
   uint4* h9 = sp + 2 * HW;
   uint4* h13 = sp + 3 * HW;
-  uint16_t* img = buf + (size_t)b * HW * cs + g * 8;
+  uint8_t* img = buf + (size_t)b * HW * cs + g * 16;
   for (int p = threadIdx.x; p < HW; p += 256) xs[p] = *(const uint4*)(img + (size_t)p * cs);
   __syncthreads();
   for (int p = threadIdx.x; p < HW; p += 256) {
     const int y = p / W, x = p - (p / W) * W;
-    float a5[8], a9[8], a13[8];
+    float a5[NV], a9[NV], a13[NV];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a5[j] = a9[j] = a13[j] = -INFINITY;
+    for (int j = 0; j < NV; ++j) a5[j] = a9[j] = a13[j] = -INFINITY;
 #pragma unroll
     for (int d = -6; d <= 6; ++d) {
       const int xx = x + d;
       if (xx < 0 || xx >= W) continue;
-      float f[8];
-      bf8_to_f(xs[y * W + xx], f);
+      float f[NV];
+      V::dec(xs[y * W + xx], f);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < NV; ++j) {
         a13[j] = fmaxf(a13[j], f[j]);
         if (d >= -4 && d <= 4) a9[j] = fmaxf(a9[j], f[j]);
         if (d >= -2 && d <= 2) a5[j] = fmaxf(a5[j], f[j]);
       }
     }
-    h5[p] = f_to_bf8(a5);
-    h9[p] = f_to_bf8(a9);
-    h13[p] = f_to_bf8(a13);
+    h5[p] = V::enc(a5);
+    h9[p] = V::enc(a9);
+    h13[p] = V::enc(a13);
   }
   __syncthreads();
   for (int p = threadIdx.x; p < HW; p += 256) {
     const int y = p / W, x = p - (p / W) * W;
-    float a5[8], a9[8], a13[8];
+    float a5[NV], a9[NV], a13[NV];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a5[j] = a9[j] = a13[j] = -INFINITY;
+    for (int j = 0; j < NV; ++j) a5[j] = a9[j] = a13[j] = -INFINITY;
 #pragma unroll
     for (int d = -6; d <= 6; ++d) {
       const int yy = y + d;
       if (yy < 0 || yy >= H) continue;
       const int q = yy * W + x;
-      float f[8];
-      bf8_to_f(h13[q], f);
+      float f[NV];
+      V::dec(h13[q], f);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) a13[j] = fmaxf(a13[j], f[j]);
+      for (int j = 0; j < NV; ++j) a13[j] = fmaxf(a13[j], f[j]);
       if (d >= -4 && d <= 4) {
-        bf8_to_f(h9[q], f);
+        V::dec(h9[q], f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a9[j] = fmaxf(a9[j], f[j]);
+        for (int j = 0; j < NV; ++j) a9[j] = fmaxf(a9[j], f[j]);
       }
       if (d >= -2 && d <= 2) {
-        bf8_to_f(h5[q], f);
+        V::dec(h5[q], f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a5[j] = fmaxf(a5[j], f[j]);
+        for (int j = 0; j < NV; ++j) a5[j] = fmaxf(a5[j], f[j]);
       }
     }
-    uint16_t* o = img + (size_t)p * cs;
-    *(uint4*)(o + c) = f_to_bf8(a5);
-    *(uint4*)(o + 2 * c) = f_to_bf8(a9);
-    *(uint4*)(o + 3 * c) = f_to_bf8(a13);
+    uint8_t* o = img + (size_t)p * cs;
+    *(uint4*)(o + c * EB) = V::enc(a5);
+    *(uint4*)(o + 2 * c * EB) = V::enc(a9);
+    *(uint4*)(o + 3 * c * EB) = V::enc(a13);
   }
 }
 
-int launch_sppf_pool(bf16_t* buf, int B, int H, int W, int c, hipStream_t s) {
+template <bool F8>
+static int launch_sppf_t(uint8_t* buf, int B, int H, int W, int c, hipStream_t s) {
   const size_t smem = (size_t)H * W * 64;  // 4 x 16 B per pixel
-  if (c % 8 != 0 || smem > kSppfLds) {
+  const int nv = F8 ? 16 : 8;
+  if (c % nv != 0 || smem > kSppfLds) {
     set_error("sppf: c=%d / map %dx%d unsupported by the LDS pool", c, H, W);
     return RV_EINVAL;
   }
   static bool attr = false;
   if (!attr && smem > 64 * 1024) {  // only raise the cap when a map needs it
     // best effort: a failure surfaces as the launch error reported below
-    (void)hipFuncSetAttribute((const void*)sppf_pool_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        kSppfLds);
+    (void)hipFuncSetAttribute((const void*)sppf_pool_kernel<F8>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLds);
     (void)hipGetLastError();
     attr = true;
   }
-  sppf_pool_kernel<<<B * (c / 8), 256, smem, s>>>(buf, B, H, W, c);
+  sppf_pool_kernel<F8><<<B * (c / nv), 256, smem, s>>>(buf, B, H, W, c);
   return launch_status("sppf_pool");
+}
+
+int launch_sppf_pool(bf16_t* buf, int B, int H, int W, int c, hipStream_t s) {
+  return launch_sppf_t<false>((uint8_t*)buf, B, H, W, c, s);
+}
+
+int launch_sppf_pool_fp8(uint8_t* buf, int B, int H, int W, int c, hipStream_t s) {
+  return launch_sppf_t<true>(buf, B, H, W, c, s);
 }
 
 // ---------------------------------------------------------------------------

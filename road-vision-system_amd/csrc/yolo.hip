@@ -22,6 +22,8 @@ struct ConvSpec {
   std::string name;
   int cin, cout, k, s, act;
   size_t w_off = 0, b_off = 0;  // byte offsets in the packed blob
+  size_t ws_off = 0;            // fp8 convs: per-cout weight scales (f32)
+  bool f8 = false;              // fp8 weights / inputs (RV_YOLO_DTYPE_FP8 plans)
 };
 
 struct Variant {
@@ -61,6 +63,7 @@ static bool variant_widths(int variant, Variant& v) {
 
 struct ModelDef {
   Variant v;
+  int dtype = 0;  // RV_YOLO_DTYPE_BF16 / RV_YOLO_DTYPE_FP8
   std::vector<ConvSpec> convs;
   int add(const std::string& n, int ci, int co, int k, int s, int act = 1) {
     ConvSpec c;
@@ -89,8 +92,10 @@ struct ModelDef {
   }
 };
 
-static bool build_def(int variant, ModelDef& m) {
+static bool build_def(int variant, ModelDef& m, int dtype = RV_YOLO_DTYPE_BF16) {
   if (!variant_widths(variant, m.v)) return false;
+  if (dtype != RV_YOLO_DTYPE_BF16 && dtype != RV_YOLO_DTYPE_FP8) return false;
+  m.dtype = dtype;
   const Variant& v = m.v;
   m.add("model.0", 3, v.c1, 3, 2);
   m.add("model.1", v.c1, v.c2, 3, 2);
@@ -123,31 +128,66 @@ static bool build_def(int variant, ModelDef& m) {
     m.add(p + ".2", v.c3d, v.nc, 1, 1, 0);
   }
   // packed layout: conv 0 keeps f32 OIHW (VALU conv), the rest bf16
-  // [Cout_pad16][ky][kx][Cin_pad32]; biases f32 [Cout_pad16]; 256-B aligned
+  // [Cout_pad16][ky][kx][Cin_pad32]; biases f32 [Cout_pad16]; 256-B aligned.
+  // fp8 plans: every conv but conv 0 and the Detect head's last 1x1 stage
+  // (run inside the decode kernel on bf16 features) is fp8 e4m3
+  // [Cout_pad16][ky][kx][Cin_pad64] + f32 per-cout scales [Cout_pad16].
   size_t off = 0;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   for (size_t i = 0; i < m.convs.size(); ++i) {
     ConvSpec& c = m.convs[i];
+    c.f8 = dtype == RV_YOLO_DTYPE_FP8 && i > 0 &&
+           !(c.name.compare(0, 9, "model.22.") == 0 && c.name.size() > 2 &&
+             c.name.compare(c.name.size() - 2, 2, ".2") == 0);
     const int cop = (c.cout + 15) & ~15;
-    const int cip = (c.cin + 31) & ~31;
+    const int cip = c.f8 ? (c.cin + 63) & ~63 : (c.cin + 31) & ~31;
     c.w_off = off;
     off = al(off + (i == 0 ? (size_t)c.cout * c.cin * c.k * c.k * 4
-                           : (size_t)cop * c.k * c.k * cip * 2));
+                           : (size_t)cop * c.k * c.k * cip * (c.f8 ? 1 : 2)));
     c.b_off = off;
     off = al(off + (size_t)cop * 4);
+    if (c.f8) {
+      c.ws_off = off;
+      off = al(off + (size_t)cop * 4);
+    }
   }
   return true;
 }
 
 static size_t packed_bytes(const ModelDef& m) {
   const ConvSpec& c = m.convs.back();
-  return ((c.b_off + (size_t)((c.cout + 15) & ~15) * 4) + 255) & ~(size_t)255;
+  const size_t last = c.f8 ? c.ws_off : c.b_off;
+  return ((last + (size_t)((c.cout + 15) & ~15) * 4) + 255) & ~(size_t)255;
 }
 
 static size_t flat_floats(const ModelDef& m) {
   size_t n = 0;
   for (const ConvSpec& c : m.convs) n += (size_t)c.cout * c.cin * c.k * c.k + c.cout;
   return n;
+}
+
+// OCP e4m3fn code of x (|x| saturated to 448, round to nearest even,
+// subnormals in 2^-9 steps) -- the rounding of v_cvt_pk_fp8_f32
+static uint8_t host_f2e4m3(float x) {
+  const uint8_t sgn = std::signbit(x) ? 0x80 : 0;
+  double a = std::fabs((double)x);
+  if (a > 448.0) a = 448.0;
+  if (a < std::ldexp(1.0, -6)) return sgn | (uint8_t)std::nearbyint(a * 512.0);  // 8 -> 2^-6
+  int e;
+  const double m = std::frexp(a, &e);  // a = m 2^e, m in [0.5, 1)
+  int q = (int)std::nearbyint((m * 2.0 - 1.0) * 8.0);
+  int E = e - 1 + 7;
+  if (q == 8) {
+    q = 0;
+    ++E;
+  }
+  return sgn | (uint8_t)((E << 3) | q);
+}
+
+// smallest power of two s with amax / s <= 448 (1 for amax == 0)
+static float pow2_scale(double amax) {
+  if (!(amax > 0.0)) return 1.0f;
+  return (float)std::ldexp(1.0, (int)std::ceil(std::log2(amax / 448.0)));
 }
 
 static uint16_t host_f2bf(float f) {
@@ -170,6 +210,7 @@ struct Buf {
   size_t elems_per_img;
   bool f32;
   size_t off_bytes;  // filled per B
+  int esize = 2;     // bytes per element: 4 (f32 logits), 2 (bf16), 1 (fp8 codes)
 };
 
 struct TraceRec {
@@ -220,6 +261,10 @@ struct Model {
     }
   }
   int max_B = 0, H = 0, W = 0;
+  // fp8 plans: per-buffer activation scales (value = code * scale), powers
+  // of two; set by rv_yolo_set_act_scales before the first forward
+  std::vector<float> act_scale;
+  bool scales_set = false;
   // RV_YOLO_OPT_RAW_UNFUSED: forwards that return the raw prediction run the
   // unfused stem, so every activation (X0 included) is in the workspace
   int raw_unfused = 1;
@@ -230,15 +275,18 @@ struct Model {
   int map_h[6], map_w[6];  // stride 2^i maps
 
   std::vector<int> buf_h, buf_w, buf_c;
-  int newbuf(int s, int c, bool f32 = false) {
+  std::vector<std::string> buf_name;
+  int newbuf(const std::string& name, int s, int c, bool f32 = false, bool bf16 = false) {
     Buf b;
     b.elems_per_img = (size_t)map_h[s] * map_w[s] * c;
     b.f32 = f32;
     b.off_bytes = 0;
+    b.esize = f32 ? 4 : (def.dtype == RV_YOLO_DTYPE_FP8 && !bf16 ? 1 : 2);
     bufs.push_back(b);
     buf_h.push_back(map_h[s]);
     buf_w.push_back(map_w[s]);
     buf_c.push_back(c);
+    buf_name.push_back(name);
     return (int)bufs.size() - 1;
   }
   // buffer ids
@@ -249,7 +297,7 @@ struct Model {
   size_t ws_bytes(int B) const {
     size_t off = 0;
     for (const Buf& b : bufs)
-      off = (off + b.elems_per_img * B * (b.f32 ? 4 : 2) + 255) & ~(size_t)255;
+      off = (off + b.elems_per_img * B * b.esize + 255) & ~(size_t)255;
     return off;
   }
 };
@@ -260,33 +308,34 @@ static void plan(Model& M) {
     M.map_h[i] = M.H >> i;
     M.map_w[i] = M.W >> i;
   }
-  M.X0 = M.newbuf(1, v.c1);
-  M.X1 = M.newbuf(2, v.c2);
-  M.C2 = M.newbuf(2, (2 + v.nb) * (v.c2 / 2));
-  M.X2 = M.newbuf(2, v.c2);
-  M.X3 = M.newbuf(3, v.c3);
-  M.C4 = M.newbuf(3, (2 + v.nm) * (v.c3 / 2));
-  M.CAT14 = M.newbuf(3, v.h12 + v.c3);
-  M.X5 = M.newbuf(4, v.c4);
-  M.C6 = M.newbuf(4, (2 + v.nm) * (v.c4 / 2));
-  M.CAT11 = M.newbuf(4, v.c5 + v.c4);
-  M.X7 = M.newbuf(5, v.c5);
-  M.C8 = M.newbuf(5, (2 + v.nb) * (v.c5 / 2));
-  M.X8 = M.newbuf(5, v.c5);
-  M.SP = M.newbuf(5, 4 * (v.c5 / 2));
-  M.CAT20 = M.newbuf(5, v.h18 + v.c5);
-  M.C12 = M.newbuf(4, (2 + v.nb) * (v.h12 / 2));
-  M.CAT17 = M.newbuf(4, v.h15 + v.h12);
-  M.C15 = M.newbuf(3, (2 + v.nb) * (v.h15 / 2));
-  M.X15 = M.newbuf(3, v.h15);
-  M.C18 = M.newbuf(4, (2 + v.nb) * (v.h18 / 2));
-  M.X18 = M.newbuf(4, v.h18);
-  M.C21 = M.newbuf(5, (2 + v.nb) * (v.h21 / 2));
-  M.X21 = M.newbuf(5, v.h21);
+  M.X0 = M.newbuf("X0", 1, v.c1);
+  M.X1 = M.newbuf("X1", 2, v.c2);
+  M.C2 = M.newbuf("C2", 2, (2 + v.nb) * (v.c2 / 2));
+  M.X2 = M.newbuf("X2", 2, v.c2);
+  M.X3 = M.newbuf("X3", 3, v.c3);
+  M.C4 = M.newbuf("C4", 3, (2 + v.nm) * (v.c3 / 2));
+  M.CAT14 = M.newbuf("CAT14", 3, v.h12 + v.c3);
+  M.X5 = M.newbuf("X5", 4, v.c4);
+  M.C6 = M.newbuf("C6", 4, (2 + v.nm) * (v.c4 / 2));
+  M.CAT11 = M.newbuf("CAT11", 4, v.c5 + v.c4);
+  M.X7 = M.newbuf("X7", 5, v.c5);
+  M.C8 = M.newbuf("C8", 5, (2 + v.nb) * (v.c5 / 2));
+  M.X8 = M.newbuf("X8", 5, v.c5);
+  M.SP = M.newbuf("SP", 5, 4 * (v.c5 / 2));
+  M.CAT20 = M.newbuf("CAT20", 5, v.h18 + v.c5);
+  M.C12 = M.newbuf("C12", 4, (2 + v.nb) * (v.h12 / 2));
+  M.CAT17 = M.newbuf("CAT17", 4, v.h15 + v.h12);
+  M.C15 = M.newbuf("C15", 3, (2 + v.nb) * (v.h15 / 2));
+  M.X15 = M.newbuf("X15", 3, v.h15);
+  M.C18 = M.newbuf("C18", 4, (2 + v.nb) * (v.h18 / 2));
+  M.X18 = M.newbuf("X18", 4, v.h18);
+  M.C21 = M.newbuf("C21", 5, (2 + v.nb) * (v.h21 / 2));
+  M.X21 = M.newbuf("X21", 5, v.h21);
   for (int i = 0; i < 3; ++i) {
-    M.DA[i] = M.newbuf(3 + i, v.c2d + v.c3d);
-    M.DB[i] = M.newbuf(3 + i, v.c2d + v.c3d);
-    M.HD[i] = M.newbuf(3 + i, 4 * v.reg + v.nc, true);
+    const std::string l = std::to_string(i);
+    M.DA[i] = M.newbuf("DA" + l, 3 + i, v.c2d + v.c3d);
+    M.DB[i] = M.newbuf("DB" + l, 3 + i, v.c2d + v.c3d, false, true);  // bf16: the decode's features
+    M.HD[i] = M.newbuf("HD" + l, 3 + i, 4 * v.reg + v.nc, true);
   }
   // one temp per bottleneck (its first conv's output): no buffer is ever
   // overwritten inside a forward, so every layer stays inspectable
@@ -299,8 +348,10 @@ static void plan(Model& M) {
                        {"model.12", 4, v.h12, v.nb}, {"model.15", 3, v.h15, v.nb},
                        {"model.18", 4, v.h18, v.nb}, {"model.21", 5, v.h21, v.nb}};
   for (const C2fDef& c : cs)
-    for (int i = 0; i < c.n; ++i)
-      M.tmps.push_back({std::string(c.p) + ".m." + std::to_string(i), M.newbuf(c.level, c.c2 / 2)});
+    for (int i = 0; i < c.n; ++i) {
+      const std::string q = std::string(c.p) + ".m." + std::to_string(i);
+      M.tmps.push_back({q, M.newbuf(q, c.level, c.c2 / 2)});
+    }
   M.nA = M.map_h[3] * M.map_w[3] + M.map_h[4] * M.map_w[4] + M.map_h[5] * M.map_w[5];
 }
 
@@ -315,6 +366,10 @@ struct Exec {
   void* ptr(int buf) const { return ws + off[buf]; }
   const bf16_t* wptr(const ConvSpec& c) const { return (const bf16_t*)(M->dev + c.w_off); }
   const float* bptr(const ConvSpec& c) const { return (const float*)(M->dev + c.b_off); }
+  const float* wsptr(const ConvSpec& c) const {
+    return c.f8 ? (const float*)(M->dev + c.ws_off) : nullptr;
+  }
+  float scale(int buf) const { return buf >= 0 ? M->act_scale[buf] : 1.0f; }
 
   int spec(const std::string& name) {
     const int idx = M->def.find(name);
@@ -361,6 +416,18 @@ struct Exec {
       a.res_co = res.co;
     }
     a.act = c.act;
+    if (c.f8) {
+      a.in8 = 1;
+      a.s_in = scale(in.buf);
+      a.wscale = wsptr(c);
+      a.out0_8 = M->bufs[o0.buf].esize == 1;
+      a.s_out0 = scale(o0.buf);
+      if (o1.buf >= 0) {
+        a.out1_8 = M->bufs[o1.buf].esize == 1;
+        a.s_out1 = scale(o1.buf);
+      }
+      if (res.buf >= 0) a.s_res = scale(res.buf);
+    }
     return a;
   }
 
@@ -399,10 +466,12 @@ struct Exec {
     const int cout1 = g2 ? a.g2_cout0 : a.Cout, cout2 = g2 ? a.Cout - a.g2_cout0 : 0;
     double in_ch = a.Cin;
     if (g2 && (a.g2_in_co != a.in_co || a.g2_Cin != a.Cin)) in_ch += a.g2_Cin;
-    const double outs = (a.out0 ? (a.out0_up ? 4 : 1) : 0) + (a.out1 ? (a.out1_up ? 4 : 1) : 0);
-    const double w = 2.0 * a.k * a.k * ((double)cout1 * a.Cin + (double)cout2 * (g2 ? a.g2_Cin : 0));
-    return px_in * in_ch * 2 + px_out * a.Cout * (a.out_f32 ? 4 : 2) * outs +
-           (a.res ? px_out * a.Cout * 2 : 0.0) + w;
+    const double eb = a.in8 ? 1.0 : 2.0;  // input / residual / weight element bytes
+    auto ob = [&](int o8) { return a.out_f32 ? 4.0 : (o8 ? 1.0 : 2.0); };
+    const double outs = (a.out0 ? (a.out0_up ? 4 : 1) * ob(a.out0_8) : 0) +
+                        (a.out1 ? (a.out1_up ? 4 : 1) * ob(a.out1_8) : 0);
+    const double w = eb * a.k * a.k * ((double)cout1 * a.Cin + (double)cout2 * (g2 ? a.g2_Cin : 0));
+    return px_in * in_ch * eb + px_out * a.Cout * outs + (a.res ? px_out * a.Cout * eb : 0.0) + w;
   }
 
   static double flops_of(const ConvSpec& c, const ConvArgs& a) {
@@ -485,6 +554,7 @@ struct Exec {
     a.g2_Cin = c2.cin;
     a.g2_w = wptr(c2);
     a.g2_bias = bptr(c2);
+    a.g2_wscale = wsptr(c2);
     launch(a, i1, fl);
   }
 
@@ -599,16 +669,27 @@ extern "C" size_t rv_yolo_flat_floats(int variant) {
   return flat_floats(m);
 }
 
-extern "C" size_t rv_yolo_packed_bytes(int variant) {
+extern "C" size_t rv_yolo_packed_bytes2(int variant, int dtype) {
   ModelDef m;
-  if (!build_def(variant, m)) return 0;
+  if (!build_def(variant, m, dtype)) return 0;
   return packed_bytes(m);
 }
 
+extern "C" size_t rv_yolo_packed_bytes(int variant) {
+  return rv_yolo_packed_bytes2(variant, RV_YOLO_DTYPE_BF16);
+}
+
+extern "C" float rv_fp8_scale(double amax) { return pow2_scale(amax); }
+
 extern "C" int rv_yolo_pack(int variant, const float* flat, size_t n, void* host_out,
                             size_t out_bytes) {
+  return rv_yolo_pack2(variant, RV_YOLO_DTYPE_BF16, flat, n, host_out, out_bytes);
+}
+
+extern "C" int rv_yolo_pack2(int variant, int dtype, const float* flat, size_t n, void* host_out,
+                             size_t out_bytes) {
   ModelDef m;
-  RV_CHECK_ARG(build_def(variant, m), "unknown variant %d", variant);
+  RV_CHECK_ARG(build_def(variant, m, dtype), "unknown variant %d / dtype %d", variant, dtype);
   RV_CHECK_ARG(flat && host_out, "null pointer");
   RV_CHECK_ARG(n == flat_floats(m), "flat weights: got %zu floats, need %zu", n, flat_floats(m));
   RV_CHECK_ARG(out_bytes >= packed_bytes(m), "packed buffer too small");
@@ -623,6 +704,24 @@ extern "C" int rv_yolo_pack(int variant, const float* flat, size_t n, void* host
     p += nw + c.cout;
     if (i == 0) {
       memcpy(out + c.w_off, w, nw * 4);
+    } else if (c.f8) {
+      // per output channel: scale = 2^ceil(log2(amax / 448)), codes RNE
+      const int cip = (c.cin + 63) & ~63;
+      const int kk = c.k * c.k;
+      uint8_t* dst = out + c.w_off;
+      float* wsc = (float*)(out + c.ws_off);
+      for (int o = 0; o < c.cout; ++o) {
+        double amax = 0.0;
+        for (size_t j = 0; j < (size_t)c.cin * kk; ++j)
+          amax = std::max(amax, (double)std::fabs(w[(size_t)o * c.cin * kk + j]));
+        const float sc = pow2_scale(amax);
+        wsc[o] = sc;
+        for (int ky = 0; ky < c.k; ++ky)
+          for (int kx = 0; kx < c.k; ++kx)
+            for (int ci = 0; ci < c.cin; ++ci)
+              dst[((size_t)o * kk + ky * c.k + kx) * cip + ci] =
+                  host_f2e4m3(w[(((size_t)o * c.cin + ci) * c.k + ky) * c.k + kx] / sc);
+      }
     } else {
       const int cip = (c.cin + 31) & ~31;
       uint16_t* dst = (uint16_t*)(out + c.w_off);
@@ -640,13 +739,18 @@ extern "C" int rv_yolo_pack(int variant, const float* flat, size_t n, void* host
 
 extern "C" int rv_yolo_create(int variant, const void* dev_packed, int max_B, int in_h, int in_w,
                               void** handle) {
+  return rv_yolo_create2(variant, RV_YOLO_DTYPE_BF16, dev_packed, max_B, in_h, in_w, handle);
+}
+
+extern "C" int rv_yolo_create2(int variant, int dtype, const void* dev_packed, int max_B, int in_h,
+                               int in_w, void** handle) {
   RV_CHECK_ARG(handle && dev_packed, "null pointer");
   RV_CHECK_ARG(max_B > 0 && in_h > 0 && in_w > 0 && in_h % 32 == 0 && in_w % 32 == 0,
                "input %dx%d must be positive multiples of 32", in_h, in_w);
   Model* M = new Model();
-  if (!build_def(variant, M->def)) {
+  if (!build_def(variant, M->def, dtype)) {
     delete M;
-    set_error("unknown variant %d", variant);
+    set_error("unknown variant %d / dtype %d", variant, dtype);
     return RV_EINVAL;
   }
   M->dev = (const uint8_t*)dev_packed;
@@ -662,8 +766,43 @@ extern "C" int rv_yolo_create(int variant, const void* dev_packed, int max_B, in
   M->H = in_h;
   M->W = in_w;
   plan(*M);
+  M->act_scale.assign(M->bufs.size(), 1.0f);
+  M->scales_set = dtype == RV_YOLO_DTYPE_BF16;
   *handle = M;
   return RV_OK;
+}
+
+extern "C" int rv_yolo_set_act_scales(void* h, const float* scales, int n) {
+  RV_CHECK_ARG(h && scales, "null pointer");
+  Model* M = (Model*)h;
+  RV_CHECK_ARG(n == (int)M->bufs.size(), "got %d scales, the plan has %d buffers", n,
+               (int)M->bufs.size());
+  for (int i = 0; i < n; ++i) {
+    if (M->bufs[i].esize != 1) continue;
+    int e;
+    const float f = std::frexp(scales[i], &e);
+    RV_CHECK_ARG(scales[i] > 0.f && std::isfinite(scales[i]) && f == 0.5f,
+                 "buffer %d: scale %g is not a positive power of two", i, (double)scales[i]);
+  }
+  for (int i = 0; i < n; ++i) M->act_scale[i] = M->bufs[i].esize == 1 ? scales[i] : 1.0f;
+  M->scales_set = true;
+  return RV_OK;
+}
+
+extern "C" int rv_yolo_buffer_name(void* h, int buf, char* name, int cap) {
+  RV_CHECK_ARG(h && name && cap > 0, "bad args");
+  Model* M = (Model*)h;
+  RV_CHECK_ARG(buf >= 0 && buf < (int)M->bufs.size(), "bad buffer %d", buf);
+  strncpy(name, M->buf_name[buf].c_str(), cap - 1);
+  name[cap - 1] = 0;
+  return RV_OK;
+}
+
+extern "C" int rv_yolo_buffer_esize(void* h, int buf) {
+  RV_CHECK_ARG(h, "null handle");
+  Model* M = (Model*)h;
+  RV_CHECK_ARG(buf >= 0 && buf < (int)M->bufs.size(), "bad buffer %d", buf);
+  return M->bufs[buf].esize;
 }
 
 extern "C" int rv_yolo_destroy(void* h) {
@@ -713,7 +852,9 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   RV_CHECK_ARG(B > 0 && B <= M->max_B, "B=%d outside (0, %d]", B, M->max_B);
   RV_CHECK_ARG(ws_bytes >= M->ws_bytes(B), "workspace %zu < %zu bytes", ws_bytes, M->ws_bytes(B));
   RV_CHECK_ARG(!cand || (cand_n && cand_cap > 0), "candidate buffers incomplete");
+  RV_CHECK_ARG(M->scales_set, "fp8 plan: activation scales not set (rv_yolo_set_act_scales)");
   const Variant& v = M->def.v;
+  const bool f8 = M->def.dtype == RV_YOLO_DTYPE_FP8;
   Exec E;
   E.M = M;
   E.ws = (uint8_t*)ws;
@@ -722,7 +863,7 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   size_t off = 0;
   for (const Buf& b : M->bufs) {
     E.off.push_back(off);
-    off = (off + b.elems_per_img * B * (b.f32 ? 4 : 2) + 255) & ~(size_t)255;
+    off = (off + b.elems_per_img * B * b.esize + 255) & ~(size_t)255;
   }
   M->trace.clear();
   M->launches.clear();
@@ -735,7 +876,7 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   static const bool stem_env = !getenv("RV_FUSE_STEM") || atoi(getenv("RV_FUSE_STEM")) != 0;
   const int i1 = M->def.find("model.1");
   const bool fuse_stem =
-      stem_env && !(raw_out && M->raw_unfused) && c0.cout == 16 && v.c2 == 32 && i1 >= 0;
+      stem_env && !f8 && !(raw_out && M->raw_unfused) && c0.cout == 16 && v.c2 == 32 && i1 >= 0;
   int st;
   if (fuse_stem) {
     const ConvSpec& c1 = M->def.convs[i1];
@@ -747,16 +888,19 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
                      (bf16_t*)E.ptr(M->X1), v.c2, E.s);
     if (st) return st;
   } else {
-    st = launch_conv0(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
-                      (const float*)(M->dev + c0.b_off), c0.cout, (bf16_t*)E.ptr(M->X0), v.c1,
-                      E.s);
+    st = f8 ? launch_conv0_fp8(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
+                               (const float*)(M->dev + c0.b_off), c0.cout, (uint8_t*)E.ptr(M->X0),
+                               v.c1, E.scale(M->X0), E.s)
+            : launch_conv0(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
+                           (const float*)(M->dev + c0.b_off), c0.cout, (bf16_t*)E.ptr(M->X0), v.c1,
+                           E.s);
     if (st) return st;
     E.conv("model.1", View{M->X0, v.c1, 0}, 1, View{M->X1, v.c2, 0});
   }
   // fused C2f chains (c2f.hip) unless a raw parity forward keeps every
   // activation (RV_YOLO_OPT_RAW_UNFUSED) or RV_FUSE_C2F=0
   static const bool c2f_env = !getenv("RV_FUSE_C2F") || atoi(getenv("RV_FUSE_C2F")) != 0;
-  const bool fuse_c2f = c2f_env && M->fuse_c2f && !(raw_out && M->raw_unfused);
+  const bool fuse_c2f = c2f_env && !f8 && M->fuse_c2f && !(raw_out && M->raw_unfused);
   E.c2f("model.2", View{M->X1, v.c2, 0}, 2, M->C2, v.c2, v.nb, true, View{M->X2, v.c2, 0}, 0,
         View{-1, 0, 0}, 0, fuse_c2f);
   E.conv("model.3", View{M->X2, v.c2, 0}, 2, View{M->X3, v.c3, 0});
@@ -773,7 +917,8 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   const int sc = v.c5 / 2;
   E.conv("model.9.cv1", View{M->X8, v.c5, 0}, 5, View{M->SP, 4 * sc, 0});
   if (E.status) return E.status;
-  st = launch_sppf_pool((bf16_t*)E.ptr(M->SP), B, M->map_h[5], M->map_w[5], sc, E.s);
+  st = f8 ? launch_sppf_pool_fp8((uint8_t*)E.ptr(M->SP), B, M->map_h[5], M->map_w[5], sc, E.s)
+          : launch_sppf_pool((bf16_t*)E.ptr(M->SP), B, M->map_h[5], M->map_w[5], sc, E.s);
   if (st) return st;
   E.conv("model.9.cv2", View{M->SP, 4 * sc, 0}, 5, View{M->CAT20, cat20, v.h18}, 0,
          View{M->CAT11, cat11, 0}, 1);
@@ -882,7 +1027,7 @@ extern "C" int rv_yolo_buffer_info(void* h, int B, int buf, int* info, size_t* o
   RV_CHECK_ARG(buf >= 0 && buf < (int)M->bufs.size(), "bad buffer %d", buf);
   size_t off = 0;
   for (int i = 0; i < buf; ++i)
-    off = (off + M->bufs[i].elems_per_img * B * (M->bufs[i].f32 ? 4 : 2) + 255) & ~(size_t)255;
+    off = (off + M->bufs[i].elems_per_img * B * M->bufs[i].esize + 255) & ~(size_t)255;
   *off_bytes = off;
   info[0] = M->buf_h[buf];
   info[1] = M->buf_w[buf];
@@ -960,7 +1105,8 @@ static size_t out_bytes(const ConvArgs& a, int d) {
   if (!p) return 0;
   const int up = d == 0 ? a.out0_up : a.out1_up;
   const int cs = d == 0 ? a.out0_cs : a.out1_cs;
-  return (size_t)a.B * a.Ho * a.Wo * (up ? 4 : 1) * cs * (a.out_f32 ? 4 : 2);
+  const int o8 = d == 0 ? a.out0_8 : a.out1_8;
+  return (size_t)a.B * a.Ho * a.Wo * (up ? 4 : 1) * cs * (a.out_f32 ? 4 : (o8 ? 1 : 2));
 }
 
 __global__ void count_diff_kernel(const uint32_t* __restrict__ x, const uint32_t* __restrict__ y,

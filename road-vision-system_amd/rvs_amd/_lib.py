@@ -80,6 +80,13 @@ _SIGS = {
     "rv_yolo_create": (c_int, [c_int, c_void_p, c_int, c_int, c_int, POINTER(c_void_p)]),
     "rv_yolo_destroy": (c_int, [c_void_p]),
     "rv_yolo_set_option": (c_int, [c_void_p, c_int, c_int]),
+    "rv_yolo_packed_bytes2": (c_size_t, [c_int, c_int]),
+    "rv_yolo_pack2": (c_int, [c_int, c_int, c_void_p, c_size_t, c_void_p, c_size_t]),
+    "rv_yolo_create2": (c_int, [c_int, c_int, c_void_p, c_int, c_int, c_int, POINTER(c_void_p)]),
+    "rv_yolo_set_act_scales": (c_int, [c_void_p, c_void_p, c_int]),
+    "rv_yolo_buffer_esize": (c_int, [c_void_p, c_int]),
+    "rv_yolo_buffer_name": (c_int, [c_void_p, c_int, ctypes.c_char_p, c_int]),
+    "rv_fp8_scale": (c_float, [c_double]),
     "rv_yolo_ws_bytes": (c_size_t, [c_void_p, c_int]),
     "rv_yolo_num_anchors": (c_int, [c_void_p]),
     "rv_yolo_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_float,
@@ -151,7 +158,7 @@ def check(status: int, what: str = "") -> None:
 
 _NOCHECK = {"rv_abi_version", "rv_cand_segments", "rv_yolo_cand_segments", "rv_clahe_median_fits", "rv_clahe_median_letterbox_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
             "rv_yolo_num_buffers", "rv_yolo_trace", "rv_yolo_profile_read", "rv_yolo_tuned_config",
-            "rv_yolo_profile_bytes"}
+            "rv_yolo_profile_bytes", "rv_yolo_buffer_esize"}
 
 
 def call(name: str, *args) -> int:

@@ -169,14 +169,20 @@ def load_weights(path: str, variant: int) -> np.ndarray:
     return flat_from_state_dict(read_state_dict(path), variant)
 
 
-def pack(variant: int, flat: np.ndarray) -> np.ndarray:
-    """Device layout (bf16 [Cout16][ky][kx][Cin32] + f32 bias) as a u8 host array."""
+DTYPES = {"bf16": 0, "fp8": 1}  # RV_YOLO_DTYPE_BF16 / RV_YOLO_DTYPE_FP8
+
+
+def pack(variant: int, flat: np.ndarray, dtype: str = "bf16") -> np.ndarray:
+    """Device layout as a u8 host array: bf16 [Cout16][ky][kx][Cin32] + f32
+    bias, or (dtype 'fp8') OCP e4m3 [Cout16][ky][kx][Cin64] + f32 bias + f32
+    per-cout power-of-two scales for every conv the fp8 plan runs in fp8."""
     lib = _lib.load()
+    dt = DTYPES[dtype]
     flat = np.ascontiguousarray(flat, np.float32)
-    nbytes = lib.rv_yolo_packed_bytes(variant)
+    nbytes = lib.rv_yolo_packed_bytes2(variant, dt)
     out = np.zeros(nbytes, np.uint8)
-    _lib.check(lib.rv_yolo_pack(variant, flat.ctypes.data, flat.size, out.ctypes.data, nbytes),
-               "rv_yolo_pack")
+    _lib.check(lib.rv_yolo_pack2(variant, dt, flat.ctypes.data, flat.size, out.ctypes.data, nbytes),
+               "rv_yolo_pack2")
     return out
 
 

@@ -22,7 +22,7 @@ from .. import _lib, kernels
 from .._lib import call, ptr, stream_ptr
 from .base import Detector
 from .types import Detection
-from .weights import COCO80, pack, variant_of, weights_from_config
+from .weights import COCO80, DTYPES, pack, variant_of, weights_from_config
 
 CAND_BYTES = 32
 
@@ -54,14 +54,25 @@ class YoloEngine:
     activation workspace; the packed weights are shared), so forwards of
     consecutive steps can run concurrently on different HIP streams -- each
     forward is a latency-bound chain of small launches that leaves most of
-    the chip idle.  Letterbox and candidate buffers have 2 * lanes slots."""
+    the chip idle.  Letterbox and candidate buffers have 2 * lanes slots.
+
+    dtype 'fp8' (BASELINE configs[4]): the conv stack runs on the fp8 MFMA
+    (OCP e4m3 weights and activations, power-of-two scales; include/rvhip.h
+    RV_YOLO_DTYPE_FP8).  Its per-buffer activation scales come from
+    `act_scales` (a saved calibration) or from calibrate(); a forward before
+    either raises."""
 
     def __init__(self, variant: int, flat_weights: np.ndarray, max_batch: int, frame_hw,
                  imgsz: int = 640, stride: int = 32, conf: float = 0.25, iou: float = 0.7,
                  max_det: int = 100, classes_keep: Sequence[int] = (), max_wh: float = 7680.0,
-                 max_nms: int = 30000, device="cuda", lanes: int = 1):
+                 max_nms: int = 30000, device="cuda", lanes: int = 1, dtype: str = "bf16",
+                 act_scales: Optional[Sequence[float]] = None):
         self.device = torch.device(device)
         self.variant = variant
+        if dtype not in DTYPES:
+            raise ValueError(f"dtype {dtype!r}: expected one of {sorted(DTYPES)}")
+        self.dtype = dtype
+        self.flat = flat_weights
         self.H, self.W = int(frame_hw[0]), int(frame_hw[1])
         self.max_batch = int(max_batch)
         self.conf, self.iou, self.max_det, self.max_wh = float(conf), float(iou), int(max_det), \
@@ -69,13 +80,13 @@ class YoloEngine:
         self.max_nms = int(max_nms)  # Ultralytics non_max_suppression default
         self.geo = kernels.letterbox_geometry(self.H, self.W, imgsz, stride)
         self.in_h, self.in_w = self.geo[0], self.geo[1]
-        self.packed = torch.from_numpy(pack(variant, flat_weights)).to(self.device)
+        self.packed = torch.from_numpy(pack(variant, flat_weights, dtype)).to(self.device)
         self.lanes = max(1, int(lanes))
         self._hs = []
         for _ in range(self.lanes):
             h = ctypes.c_void_p()
-            call("rv_yolo_create", variant, ptr(self.packed), self.max_batch, self.in_h,
-                 self.in_w, ctypes.byref(h))
+            call("rv_yolo_create2", variant, DTYPES[dtype], ptr(self.packed), self.max_batch,
+                 self.in_h, self.in_w, ctypes.byref(h))
             self._hs.append(h)
         self._h = h = self._hs[0]
         lib = _lib.load()
@@ -112,6 +123,62 @@ class YoloEngine:
         self.scale5 = torch.tensor([gain, px, py, self.W, self.H], dtype=torch.float32, device=dev)
         m = class_mask(classes_keep)
         self.keep = None if m is None else torch.from_numpy(m.view(np.int32)).to(dev)
+        self.act_scales = None
+        if act_scales is not None:
+            self.set_act_scales(act_scales)
+
+    def buffers(self, B: int, h=None):
+        """Activation buffers of the plan for batch B: [(name, H, W, C,
+        element bytes, byte offset in the workspace)]."""
+        lib = _lib.load()
+        h = self._h if h is None else h
+        out = []
+        for i in range(lib.rv_yolo_num_buffers(h)):
+            info = (ctypes.c_int * 4)()
+            off = ctypes.c_size_t()
+            call("rv_yolo_buffer_info", h, B, i, info, ctypes.byref(off))
+            name = ctypes.create_string_buffer(64)
+            call("rv_yolo_buffer_name", h, i, name, 64)
+            out.append((name.value.decode(), info[0], info[1], info[2],
+                        lib.rv_yolo_buffer_esize(h, i), off.value))
+        return out
+
+    def set_act_scales(self, scales: Sequence[float]) -> None:
+        """Per-buffer fp8 activation scales (powers of two; the order of
+        buffers())."""
+        arr = (ctypes.c_float * len(scales))(*[float(x) for x in scales])
+        for h in self._hs:
+            call("rv_yolo_set_act_scales", h, arr, len(scales))
+        self.act_scales = [float(x) for x in scales]
+
+    def calibrate(self, lb: torch.Tensor) -> List[float]:
+        """fp8 plans: one power-of-two scale per activation buffer, from the
+        absolute maximum the bf16 plan of the same weights reaches in that
+        buffer on this letterboxed batch (rv_fp8_scale: amax / scale in
+        (224, 448]); installs and returns them."""
+        lib = _lib.load()
+        B = lb.shape[0]
+        packed = torch.from_numpy(pack(self.variant, self.flat, "bf16")).to(self.device)
+        h = ctypes.c_void_p()
+        call("rv_yolo_create2", self.variant, 0, ptr(packed), B, self.in_h, self.in_w,
+             ctypes.byref(h))
+        try:
+            ws = torch.empty(lib.rv_yolo_ws_bytes(h, B), dtype=torch.uint8, device=self.device)
+            raw = torch.empty((B, 4 + self.nc, self.A), dtype=torch.float32, device=self.device)
+            # raw forward with RV_YOLO_OPT_RAW_UNFUSED (default): every buffer written
+            call("rv_yolo_forward", h, ptr(lb.contiguous()), B, ptr(ws), ws.numel(), ptr(raw),
+                 self.conf, None, 0, None, stream_ptr())
+            scales = []
+            for name, H, W, C, es, off in self.buffers(B, h):
+                n = B * H * W * C
+                v = ws[off:off + n * es].view(torch.float32 if es == 4 else torch.bfloat16)
+                amax = float(v.float().abs().max().item()) if n else 0.0
+                scales.append(float(lib.rv_fp8_scale(amax)))
+            torch.cuda.synchronize(self.device)
+        finally:
+            lib.rv_yolo_destroy(h)
+        self.set_act_scales(scales)
+        return scales
 
     def close(self):
         for h in getattr(self, "_hs", []):
