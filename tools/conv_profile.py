@@ -14,10 +14,13 @@ B = int(os.environ.get("B", 32))
 H, W = int(os.environ.get("H", 1080)), int(os.environ.get("W", 1920))
 V = int(os.environ.get("V", 0))
 N = int(os.environ.get("N", 10))
+DT = os.environ.get("DTYPE", "bf16")
 flat = weights.synthetic_weights(V)
-eng = YoloEngine(V, flat, B, (H, W))
+eng = YoloEngine(V, flat, B, (H, W), imgsz=int(os.environ.get("IMGSZ", 640)), dtype=DT)
 x = (torch.rand((B, H, W, 3), device="cuda") * 255).to(torch.uint8)
 lb = eng.letterbox(x)
+if DT == "fp8":
+    eng.calibrate(lb)
 for _ in range(3):
     eng.forward_raw(lb)
 if not os.environ.get("NO_TUNE"):
@@ -38,13 +41,14 @@ nf = lib.rv_yolo_profile_read(eng._h, ms.ctypes.data, fl.ctypes.data, cv.ctypes.
 convs = weights.conv_list(V)
 tot = 0
 rows = []
+cfgs = eng.tuned_configs()
 for i in range(n):
     if cv[i] < 0:
         continue
     name, ci, co, k, st, act = convs[cv[i]]
     t = ms[i] / nf
     tot += t
-    rows.append((t, name, ci, co, k, st, fl[i]))
-print(f"B={B} {H}x{W} forward {fwd:.3f} ms (events), conv sum {tot:.3f} ms over {len(rows)} launches")
-for t, name, ci, co, k, st, f in (rows if os.environ.get("ORDER") else sorted(rows, reverse=True)[:40]):
-    print(f"{t*1e3:8.1f} us {f/1e9:7.2f} GF {f/t/1e9:7.1f} TF/s  {name:22s} {ci:4d}->{co:4d} k{k} s{st}")
+    rows.append((t, name, ci, co, k, st, fl[i], cfgs[i] if i < len(cfgs) else ()))
+print(f"{DT} B={B} {H}x{W} forward {fwd:.3f} ms (events), conv sum {tot:.3f} ms over {len(rows)} launches")
+for t, name, ci, co, k, st, f, c in (rows if os.environ.get("ORDER") else sorted(rows, reverse=True)[:40]):
+    print(f"{t*1e3:8.1f} us {f/1e9:7.2f} GF {f/t/1e9:7.1f} TF/s  {name:22s} {ci:4d}->{co:4d} k{k} s{st}  cfg {c}")

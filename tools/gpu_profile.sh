@@ -14,4 +14,6 @@ KT=$(find "$OUT/raw" -name "*kernel_trace.csv" | head -1)
 ST=$(find "$OUT/raw" -name "*kernel_stats.csv" | head -1)
 cp "$ST" "$OUT/rocprof_kernel_stats_whole_run.csv"
 python3 tools/trace_window.py "$KT" "$STEPS" "$OUT/timed" || exit $?
+python3 tools/stream_busy.py "$KT" "$STEPS" > "$OUT/timed_streams.txt" || exit $?
+gzip -c "$KT" > "$OUT/kernel_trace.csv.gz"
 rm -rf "$OUT/raw"
