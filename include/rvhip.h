@@ -163,6 +163,10 @@ int rv_yolo_destroy(void* handle);
  * launch for the bottlenecks and cv2 (bit-identical to the unfused convs);
  * 0: one launch per conv. */
 #define RV_YOLO_OPT_FUSE_C2F 2
+/* RV_YOLO_OPT_STEM_X1 (default 0): the fused stem (conv0 + model.1, and
+ * model.2.cv1 from its registers) also writes the X1 map; by default X1
+ * never reaches HBM when model.2.cv1 is fused. */
+#define RV_YOLO_OPT_STEM_X1 3
 int rv_yolo_set_option(void* handle, int opt, int value);
 
 /* fp8 plans (BASELINE configs[4]: "YOLOv8m 1280x1280 fp8 MFMA conv path").

@@ -80,11 +80,14 @@ int launch_conv0_fp8(const uint8_t* img, int B, int H, int W, const float* w, co
                      int C0, uint8_t* out, int out_cs, float s_out, hipStream_t s);
 
 // conv0 and model.1 (C0 = 16 -> C1 = 32, k3 s2) fused: the P1 map never
-// leaves LDS.  w1/b1: model.1's packed weights / bias; out: X1 (NHWC,
-// channel stride out_cs).
+// leaves LDS.  w1/b1: model.1's packed weights / bias; out (nullable): X1
+// (NHWC, channel stride out_cs).  w2/b2/out2 (nullable): the following 1x1
+// conv 32 -> 32 (model.2.cv1) run from the registers into out2 (channel
+// stride out2_cs), bit-identical to the unfused 1x1 kernels.
 int launch_stem(const uint8_t* img, int B, int H, int W, const float* w0, const float* b0, int C0,
                 const bf16_t* w1, const float* b1, int C1, bf16_t* out, int out_cs,
-                hipStream_t s);
+                hipStream_t s, const bf16_t* w2 = nullptr, const float* b2 = nullptr,
+                bf16_t* out2 = nullptr, int out2_cs = 0);
 
 // SPPF pooling: buf holds x in channels [0, c); writes maxpool5, maxpool5^2
 // and maxpool5^3 (= clipped 5/9/13 windows) into [c,2c), [2c,3c), [3c,4c).

@@ -1416,12 +1416,23 @@ constexpr int kStLS = kStLC * 3 + 5;                    // lb row stride (bytes)
 constexpr int kStXB = kStXR * kStXC * 32;               // X0 tile bytes (35,904)
 constexpr int kStLB = kStLR * kStLS;                    // lb tile bytes (14,140)
 
+//
+// With the next 1x1 conv fused (cv1: 32 -> 32, model.2.cv1 of YOLOv8n), the
+// model.1 output channels are computed in the order that leaves lane quad q
+// holding channels 8q .. 8q+7 of its pixel (fragment m, row 4q'+i = channel
+// 8q' + 4m + i): exactly the B operand of a K = 32 MFMA in natural k order,
+// so cv1 runs straight from the registers with the operands (and k order)
+// of the unfused 1x1 kernels -- bit-identical -- and X1 never reaches HBM
+// (out == nullptr; out != nullptr still writes it, for parity tests).
 __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ img, int B, int H,
                                                    int W, const float* __restrict__ w0,
                                                    const float* __restrict__ b0,
                                                    const uint16_t* __restrict__ w1,
                                                    const float* __restrict__ b1,
-                                                   uint16_t* __restrict__ out, int out_cs) {
+                                                   uint16_t* __restrict__ out, int out_cs,
+                                                   const uint16_t* __restrict__ w2,
+                                                   const float* __restrict__ b2,
+                                                   uint16_t* __restrict__ out2, int out2_cs) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* xs = smem;                               // X0 tile: [17][66] px x 32 B
   uint8_t* ls = smem + kStXB;                       // lb tile: [35][404] u8
@@ -1558,7 +1569,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
       const int kx = 2 * p + (quad >> 1);  // quads 0,1: tap 2p; quads 2,3: tap 2p+1
 #pragma unroll
       for (int m = 0; m < MR; ++m) {
-        const int co = m * 16 + col;
+        const int co = 8 * (col >> 2) + 4 * m + (col & 3);  // row col of fragment m
         uint4 v = make_uint4(0, 0, 0, 0);
         if (kx < 3) v = *(const uint4*)(w1 + ((size_t)co * 9 + ky * 3 + kx) * 32 + (quad & 1) * 8);
         A[m] = __builtin_bit_cast(bf16x8, v);
@@ -1572,27 +1583,62 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
         for (int n = 0; n < NR; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[m], Bf[n], acc[m][n], 0, 0, 0);
     }
-  // epilogue: bias + SiLU -> X1 (bf16 NHWC, channel stride out_cs)
+  // epilogue: bias + SiLU -> X1 values (bf16); lane quad q of fragment m
+  // holds channels 8q + 4m .. 8q + 4m + 3
+  bf16x8 x1[NR];
 #pragma unroll
-  for (int n = 0; n < NR; ++n) {
-    const int oy = oy0 + 2 * wave + (n >> 1), ox = ox0 + (n & 1) * 16 + col;
-    if (oy >= H1 || ox >= W1) continue;
-    uint16_t* o = out + (((size_t)b * H1 + oy) * W1 + ox) * out_cs;
+  for (int m = 0; m < MR; ++m) {
+    const f32x4 bb = *(const f32x4*)(b1 + 8 * quad + 4 * m);
 #pragma unroll
-    for (int m = 0; m < MR; ++m) {
-      const int co = m * 16 + quad * 4;
-      const f32x4 bb = *(const f32x4*)(b1 + co);
-      *(uint2*)(o + co) = make_uint2(pack_bf16x2(silu(acc[m][n][0] + bb[0]), silu(acc[m][n][1] + bb[1])),
-                                     pack_bf16x2(silu(acc[m][n][2] + bb[2]), silu(acc[m][n][3] + bb[3])));
+    for (int n = 0; n < NR; ++n) {
+      const uint32_t lo = pack_bf16x2(silu(acc[m][n][0] + bb[0]), silu(acc[m][n][1] + bb[1]));
+      const uint32_t hi = pack_bf16x2(silu(acc[m][n][2] + bb[2]), silu(acc[m][n][3] + bb[3]));
+      x1[n][4 * m] = __builtin_bit_cast(__bf16, (uint16_t)(lo & 0xFFFF));
+      x1[n][4 * m + 1] = __builtin_bit_cast(__bf16, (uint16_t)(lo >> 16));
+      x1[n][4 * m + 2] = __builtin_bit_cast(__bf16, (uint16_t)(hi & 0xFFFF));
+      x1[n][4 * m + 3] = __builtin_bit_cast(__bf16, (uint16_t)(hi >> 16));
+    }
+  }
+  if (out) {  // X1 (bf16 NHWC, channel stride out_cs)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      const int oy = oy0 + 2 * wave + (n >> 1), ox = ox0 + (n & 1) * 16 + col;
+      if (oy >= H1 || ox >= W1) continue;
+      *(uint4*)(out + (((size_t)b * H1 + oy) * W1 + ox) * out_cs + 8 * quad) =
+          __builtin_bit_cast(uint4, x1[n]);
+    }
+  }
+  if (out2) {  // the fused 1x1 conv (32 -> 32) from the registers
+    bf16x8 A2[2];
+    f32x4 bb2[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      A2[m] = __builtin_bit_cast(bf16x8, *(const uint4*)(w2 + (m * 16 + col) * 32 + quad * 8));
+      bb2[m] = *(const f32x4*)(b2 + m * 16 + quad * 4);
+    }
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      const int oy = oy0 + 2 * wave + (n >> 1), ox = ox0 + (n & 1) * 16 + col;
+      f32x4 d[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+        d[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2[m], x1[n], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      if (oy >= H1 || ox >= W1) continue;
+      uint16_t* o = out2 + (((size_t)b * H1 + oy) * W1 + ox) * out2_cs;
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+        *(uint2*)(o + m * 16 + quad * 4) =
+            make_uint2(pack_bf16x2(silu(d[m][0] + bb2[m][0]), silu(d[m][1] + bb2[m][1])),
+                       pack_bf16x2(silu(d[m][2] + bb2[m][2]), silu(d[m][3] + bb2[m][3])));
     }
   }
 }
 
 int launch_stem(const uint8_t* img, int B, int H, int W, const float* w0, const float* b0, int C0,
                 const bf16_t* w1, const float* b1, int C1, bf16_t* out, int out_cs,
-                hipStream_t s) {
-  if (C0 != 16 || C1 != 32) {
-    set_error("stem: C0=%d C1=%d (fused stem needs 16 -> 32)", C0, C1);
+                hipStream_t s, const bf16_t* w2, const float* b2, bf16_t* out2, int out2_cs) {
+  if (C0 != 16 || C1 != 32 || (!out && !out2) || (out2 && (!w2 || !b2))) {
+    set_error("stem: C0=%d C1=%d (fused stem needs 16 -> 32) / outputs", C0, C1);
     return RV_EINVAL;
   }
   const int H0 = (H + 1) / 2, W0 = (W + 1) / 2;
@@ -1608,7 +1654,8 @@ int launch_stem(const uint8_t* img, int B, int H, int W, const float* w0, const 
     attr = true;
   }
   stem_kernel<<<blocks, 256, smem, s>>>(img, B, H, W, w0, b0, (const uint16_t*)w1, b1,
-                                        (uint16_t*)out, out_cs);
+                                        (uint16_t*)out, out_cs, (const uint16_t*)w2, b2,
+                                        (uint16_t*)out2, out2_cs);
   return launch_status("stem");
 }
 

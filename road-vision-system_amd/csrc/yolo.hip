@@ -270,6 +270,8 @@ struct Model {
   int raw_unfused = 1;
   // RV_YOLO_OPT_FUSE_C2F: narrow C2f blocks as cv1 + one fused chain launch
   int fuse_c2f = 1;
+  // RV_YOLO_OPT_STEM_X1: the fused stem also writes X1 (parity tests)
+  int stem_x1 = 0;
   std::vector<Buf> bufs;
   int nA = 0;
   int map_h[6], map_w[6];  // stride 2^i maps
@@ -562,10 +564,11 @@ struct Exec {
   // `fuse`, narrow blocks run cv1 and then one fused launch for the
   // bottlenecks + cv2 (c2f.hip; intermediates stay in LDS).
   void c2f(const std::string& p, View in, int li, int cb, int c2, int n, bool shortcut, View o0,
-           int up0 = 0, View o1 = {-1, 0, 0}, int up1 = 0, bool fuse = false) {
+           int up0 = 0, View o1 = {-1, 0, 0}, int up1 = 0, bool fuse = false,
+           bool cv1_done = false) {
     const int c = c2 / 2;
     const int cs = (2 + n) * c;
-    conv(p + ".cv1", in, li, View{cb, cs, 0});
+    if (!cv1_done) conv(p + ".cv1", in, li, View{cb, cs, 0});
     if (fuse && !status && up0 == 0 && o1.buf < 0 && c2f_fusable(c, n, cs, 0, o0.cs, o0.co)) {
       Model::FusedC2f f;
       memset(&f.a, 0, sizeof(f.a));
@@ -820,6 +823,9 @@ extern "C" int rv_yolo_set_option(void* h, int opt, int value) {
     case RV_YOLO_OPT_FUSE_C2F:
       M->fuse_c2f = value != 0;
       return RV_OK;
+    case RV_YOLO_OPT_STEM_X1:
+      M->stem_x1 = value != 0;
+      return RV_OK;
     default:
       set_error("unknown yolo option %d", opt);
       return RV_EINVAL;
@@ -878,14 +884,26 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   const bool fuse_stem =
       stem_env && !f8 && !(raw_out && M->raw_unfused) && c0.cout == 16 && v.c2 == 32 && i1 >= 0;
   int st;
+  // the fused stem also runs model.2.cv1 (32 -> 32 1x1) from its registers
+  // into the model.2 concat buffer when the shapes allow
+  const int i2cv1 = M->def.find("model.2.cv1");
+  const int c2cs = (2 + v.nb) * (v.c2 / 2);
+  const bool stem_cv1 = fuse_stem && i2cv1 >= 0 && M->def.convs[i2cv1].cin == 32 &&
+                        M->def.convs[i2cv1].cout == 32 && M->def.convs[i2cv1].k == 1;
   if (fuse_stem) {
     const ConvSpec& c1 = M->def.convs[i1];
     const View none{-1, 0, 0};
     E.trace(i1, E.args(c1, View{M->X0, v.c1, 0}, 1, View{M->X1, v.c2, 0}, 0, none, 0, none),
             View{M->X0, v.c1, 0}, View{M->X1, v.c2, 0}, 0, none, 0, none);
+    const ConvSpec* cv = stem_cv1 ? &M->def.convs[i2cv1] : nullptr;
+    if (cv)
+      E.trace(i2cv1, E.args(*cv, View{M->X1, v.c2, 0}, 2, View{M->C2, c2cs, 0}, 0, none, 0, none),
+              View{M->X1, v.c2, 0}, View{M->C2, c2cs, 0}, 0, none, 0, none);
     st = launch_stem(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
                      (const float*)(M->dev + c0.b_off), c0.cout, E.wptr(c1), E.bptr(c1), c1.cout,
-                     (bf16_t*)E.ptr(M->X1), v.c2, E.s);
+                     (!cv || M->stem_x1) ? (bf16_t*)E.ptr(M->X1) : nullptr, v.c2, E.s,
+                     cv ? E.wptr(*cv) : nullptr, cv ? E.bptr(*cv) : nullptr,
+                     cv ? (bf16_t*)E.ptr(M->C2) : nullptr, c2cs);
     if (st) return st;
   } else {
     st = f8 ? launch_conv0_fp8(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
@@ -902,7 +920,7 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   static const bool c2f_env = !getenv("RV_FUSE_C2F") || atoi(getenv("RV_FUSE_C2F")) != 0;
   const bool fuse_c2f = c2f_env && !f8 && M->fuse_c2f && !(raw_out && M->raw_unfused);
   E.c2f("model.2", View{M->X1, v.c2, 0}, 2, M->C2, v.c2, v.nb, true, View{M->X2, v.c2, 0}, 0,
-        View{-1, 0, 0}, 0, fuse_c2f);
+        View{-1, 0, 0}, 0, fuse_c2f, stem_cv1);
   E.conv("model.3", View{M->X2, v.c2, 0}, 2, View{M->X3, v.c3, 0});
   const int cat14 = v.h12 + v.c3, cat11 = v.c5 + v.c4, cat20 = v.h18 + v.c5,
             cat17 = v.h15 + v.h12;

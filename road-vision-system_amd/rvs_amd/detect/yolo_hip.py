@@ -200,6 +200,12 @@ class YoloEngine:
         for h in self._hs:
             call("rv_yolo_set_option", h, 1, 0 if fused else 1)
 
+    def set_stem_x1(self, on: bool) -> None:
+        """The fused stem also writes the X1 map (RV_YOLO_OPT_STEM_X1; by
+        default X1 stays in registers when model.2.cv1 is fused into it)."""
+        for h in self._hs:
+            call("rv_yolo_set_option", h, 3, 1 if on else 0)
+
     def set_fuse_c2f(self, on: bool) -> None:
         """Narrow C2f blocks as one fused launch (default) or one launch per
         conv (RV_YOLO_OPT_FUSE_C2F; bit-identical results)."""

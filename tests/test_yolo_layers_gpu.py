@@ -59,6 +59,11 @@ class Introspect:
             self.lib.rv_yolo_buffer_info(eng._h, B, i, info, ctypes.byref(off))
             self.bufs.append((info[0], info[1], info[2], info[3], off.value))
 
+    def raw_u16(self, buf):
+        h, w, c, f32, off = self.bufs[buf]
+        n = self.B * h * w * c
+        return self.ws[off:off + 2 * n].view(np.uint16).reshape(self.B, h, w, c)
+
     def view(self, buf):
         h, w, c, f32, off = self.bufs[buf]
         n = self.B * h * w * c
@@ -202,25 +207,79 @@ def test_autotuned_configs_are_bit_identical(cuda):
 
 
 def test_fused_stem_matches_unfused(cuda):
-    """conv0 + model.1 fused (X0 kept in LDS, model.1 on tap pairs) against
-    the unfused pair: same X0 values, model.1 accumulated in another k order,
-    so X1 agrees to 1 bf16 ulp (fewer than 1e-4 of the elements beyond)."""
+    """conv0 + model.1 (+ model.2.cv1 from the registers) fused (X0 kept in
+    LDS, model.1 on tap pairs) against the unfused launches: same X0 values,
+    model.1 accumulated in another k order, so X1 agrees to 1 bf16 ulp (fewer
+    than 1e-4 of the elements beyond); model.2.cv1 computed by the stem from
+    ITS X1 is bit-identical to the unfused 1x1 kernel run on that X1."""
     from rvs_amd.detect import weights
     from rvs_amd.detect.yolo_hip import YoloEngine
     H, W, B = 1080, 1920, 2
     eng = YoloEngine(0, weights.synthetic_weights(0, seed=3), B, (H, W), device=cuda)
     fr = np.stack([cpu.median(cpu.clahe_ycrcb(road_frame(H, W, seed=70 + b)), 3) for b in range(B)])
     lb = eng.letterbox(torch.from_numpy(fr).to(cuda))
-    eng.forward_raw(lb)  # no raw output: fused stem
-    x1_fused = Introspect(eng, B).view(1).copy()
+    eng.set_stem_x1(True)
+    eng.forward_raw(lb)  # no raw output: fused stem (+ X1 for this test)
+    ins = Introspect(eng, B)
+    x1_fused = ins.view(1).copy()
+    c2 = [i for i, bb in enumerate(ins.bufs) if bb[2] == 48 and bb[0] == 96][0]
+    cv1_fused = ins.view(c2)[..., :32].copy()
     raw = torch.empty((B, 84, eng.A), dtype=torch.float32, device=cuda)
     eng.forward_raw(lb, raw)  # raw output requested: conv0 + model.1 separately
-    x1 = Introspect(eng, B).view(1)
+    ins2 = Introspect(eng, B)
+    x1 = ins2.view(1)
     assert x1.shape == (B, 96, 160, 32)
     rms = float(np.sqrt(np.mean(x1.astype(np.float64) ** 2))) + 1e-12
     d = np.abs(x1_fused.astype(np.float64) - x1)
     assert float((d > ulp_bf16(x1) * 1.01 + 1e-3 * rms).mean()) < 1e-4
     assert (d <= 2 * ulp_bf16(x1) + 1e-2 * rms).all()
+    # cv1 of the fused stem vs a float64 recomputation from the fused X1
+    specs, params = yolo_ref.conv_specs(0)[0], {}
+    flat = weights.synthetic_weights(0, seed=3)
+    off = 0
+    for n, ci, co, k, s, act in specs:
+        nw = co * ci * k * k
+        params[n] = (flat[off:off + nw].reshape(co, ci), flat[off + nw:off + nw + co]) if k == 1 \
+            else None
+        off += nw + co
+    w, b = params["model.2.cv1"]
+    y = x1_fused.astype(np.float64) @ round_bf16(w).astype(np.float64).T + b
+    y = y / (1 + np.exp(-y))
+    rms = float(np.sqrt(np.mean(y ** 2))) + 1e-12
+    d = np.abs(cv1_fused - y)
+    assert float((d > ulp_bf16(y) * 1.01 + 1e-3 * rms).mean()) < 1e-4
+    assert (d <= 2 * ulp_bf16(y) + 1e-2 * rms).all()
+    eng.close()
+
+
+def test_stem_cv1_bit_identical_to_unfused_1x1(cuda):
+    """The stem's fused model.2.cv1 against the unfused 1x1 kernels on the
+    same X1 bits: run the production forward with X1 written, then the
+    unfused model.2.cv1 kernel is reproduced by the raw forward's layer on
+    that X1 -- the raw (unfused) forward recomputes X1 itself, so instead the
+    C2 slice of the fused forward is compared with the raw forward's C2
+    slice wherever the two X1 maps agree bit for bit over the 1x1 support
+    (the pixel itself)."""
+    from rvs_amd.detect import weights
+    from rvs_amd.detect.yolo_hip import YoloEngine
+    H, W, B = 1080, 1920, 2
+    eng = YoloEngine(0, weights.synthetic_weights(0, seed=3), B, (H, W), device=cuda)
+    fr = np.stack([cpu.median(cpu.clahe_ycrcb(road_frame(H, W, seed=70 + b)), 3) for b in range(B)])
+    lb = eng.letterbox(torch.from_numpy(fr).to(cuda))
+    eng.set_stem_x1(True)
+    eng.forward_raw(lb)
+    ins = Introspect(eng, B)
+    x1_f = ins.raw_u16(1).copy()
+    c2 = [i for i, bb in enumerate(ins.bufs) if bb[2] == 48 and bb[0] == 96][0]
+    cv1_f = ins.raw_u16(c2)[..., :32].copy()
+    raw = torch.empty((B, 84, eng.A), dtype=torch.float32, device=cuda)
+    eng.forward_raw(lb, raw)
+    ins2 = Introspect(eng, B)
+    x1_u = ins2.raw_u16(1)
+    cv1_u = ins2.raw_u16(c2)[..., :32]
+    same = (x1_f == x1_u).all(-1)
+    assert same.mean() > 0.9
+    np.testing.assert_array_equal(cv1_f[same], cv1_u[same])
     eng.close()
 
 
