@@ -74,8 +74,10 @@ def parse_args(argv=None):
                          "every conv launch while the timed region's multi-stream schedule runs "
                          "eagerly (overlap: same concurrency as the graphs), a plain sequential "
                          "eager pass, or none")
-    ap.add_argument("--depth", type=int, default=int(os.environ.get("RV_PIPE_DEPTH", 3)),
-                    help="pipelined steps: 3 = Y(k) || P(k+1) || T(k-1), 2 = [T(k-1) || P(k)] -> Y(k)")
+    ap.add_argument("--depth", type=int, default=int(os.environ.get("RV_PIPE_DEPTH", 4)),
+                    help="pipelined steps: 4 = Y2(k-1) || P(k+1) || Y1(k) || T(k-2) (the forward "
+                         "split in two halves on two forward lanes), 3 = Y(k) || P(k+1) || T(k-1), "
+                         "2 = [T(k-1) || P(k)] -> Y(k)")
     ap.add_argument("--graph-chunk", type=int, default=None,
                     help="pipeline steps per captured graph (default 8, RV_GRAPH_CHUNK; 0 = all)")
     ap.add_argument("--lanes", type=int, default=int(os.environ.get("RV_LANES", 1)),
@@ -96,8 +98,10 @@ class BenchJob:
         self.args, self.dev = args, dev
         self.cfg = bench_config()
         self.S, self.K, self.Wm = args.streams, args.steps, args.warmup
+        # depth 4 runs the two halves of consecutive forwards on two lanes
+        lanes = 2 if args.depth == 4 and not args.no_pipeline and not args.eager else args.lanes
         self.eng = RoadVisionEngine(self.cfg, self.S, (H, W), device=dev, tmax=args.tmax,
-                                    lanes=args.lanes)
+                                    lanes=lanes)
         self.frames = road_frames(self.S, self.Wm + self.K, H, W, device=dev,
                                   stream_offset=rank_streams(self.S, rank).start)
         self.ts = torch.tensor([[f / 30.0] * self.S for f in range(self.Wm + self.K)],
@@ -376,7 +380,12 @@ def main(argv=None):
                                      (not args.no_autotune)),
                    "execution": "eager" if args.eager else
                                 ("graph per step" if args.no_pipeline else
-                                 (f"graphs, dependency-graph pipeline with {args.lanes} concurrent "
+                                 ("graphs, 4-stage software pipeline: stage k runs the second "
+                                  "half of step k-1's forward || preprocess of step k+1 || the "
+                                  "first half of step k's forward || NMS+SORT+hand-back of step "
+                                  f"k-2 (two forward workspaces), {chunk_desc} steps per graph"
+                                  if args.depth == 4 else
+                                  f"graphs, dependency-graph pipeline with {args.lanes} concurrent "
                                   "YOLO forwards (preprocess runs ahead, NMS+SORT+hand-back "
                                   f"follows in step order), {chunk_desc} steps per graph"
                                   if args.lanes > 1 else

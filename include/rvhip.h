@@ -211,6 +211,16 @@ int rv_yolo_cand_segments(void* handle);
 int rv_yolo_forward(void* handle, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
                     float* raw_out, float conf, void* cand, int cand_cap, int* cand_n,
                     void* stream);
+/* The forward in two parts: part 1 = stem .. model.15 (lb used), part 2 =
+ * the bottom-up neck, the Detect heads and the decode (lb unused; reads part
+ * 1's activations from the same workspace; cand / raw as above; raw_out
+ * only with part 0 = the whole forward).  Part 2 needs a part 0 or part 1
+ * forward of the same handle before it (launch numbering of the autotuned
+ * configurations).  With two handles + workspaces a pipelined caller runs
+ * part 2 of step j-1 beside part 1 of step j. */
+int rv_yolo_forward_part(void* handle, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
+                         float* raw_out, float conf, void* cand, int cand_cap, int* cand_n,
+                         void* stream, int part);
 
 /* Introspection for layer-wise parity tests: activation buffers (NHWC,
  * info = {H, W, C, is_f32}, byte offset inside the workspace for batch B)

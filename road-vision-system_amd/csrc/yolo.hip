@@ -261,6 +261,9 @@ struct Model {
     }
   }
   int max_B = 0, H = 0, W = 0;
+  // forward parts (rv_yolo_forward_part): launch index base of this call
+  // (part 2 continues part 1's launch numbering) and part 1's launch count
+  int li_base = 0, n_part1 = -1;
   // fp8 plans: per-buffer activation scales (value = code * scale), powers
   // of two; set by rv_yolo_set_act_scales before the first forward
   std::vector<float> act_scale;
@@ -484,7 +487,7 @@ struct Exec {
   // there is a valid one, else the default; live HIP-event timing when
   // profiling is on.
   void launch(const ConvArgs& a, int idx, double flops) {
-    const int li_ = (int)M->launches.size();
+    const int li_ = M->li_base + (int)M->launches.size();
     M->launches.push_back(a);
     Profile& P = M->prof;
     const bool rec = P.on && P.n_fwd < P.cap_fwd && li_ < P.per_fwd;
@@ -850,11 +853,32 @@ extern "C" int rv_yolo_cand_segments(void* h) {
   return decode_segments(hl, 3);
 }
 
+extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
+                                    float* raw_out, float conf, void* cand, int cand_cap,
+                                    int* cand_n, void* stream, int part);
+
 extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
                                float* raw_out, float conf, void* cand, int cand_cap, int* cand_n,
                                void* stream) {
-  RV_CHECK_ARG(h && lb && ws, "null pointer");
+  return rv_yolo_forward_part(h, lb, B, ws, ws_bytes, raw_out, conf, cand, cand_cap, cand_n, stream,
+                              0);
+}
+
+// part 0: the whole forward.  part 1: stem .. model.15 (the backbone and the
+// top-down neck: the bandwidth-heavy P2/P3 layers).  part 2: the rest (the
+// bottom-up neck, the Detect heads and the decode: small latency-bound
+// launches), reading part 1's activations from the same workspace.  A
+// pipelined caller with two workspaces runs part 2 of step j-1 beside
+// part 1 of step j.
+extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
+                                    float* raw_out, float conf, void* cand, int cand_cap,
+                                    int* cand_n, void* stream, int part) {
+  RV_CHECK_ARG(h && ws && (lb || part == 2), "null pointer");
+  RV_CHECK_ARG(part >= 0 && part <= 2, "part %d not in {0, 1, 2}", part);
   Model* M = (Model*)h;
+  RV_CHECK_ARG(part != 2 || M->n_part1 >= 0,
+               "forward part 2 before any part 0 / part 1 forward of this handle");
+  RV_CHECK_ARG(part != 1 || !raw_out, "raw_out needs the whole forward (part 0)");
   RV_CHECK_ARG(B > 0 && B <= M->max_B, "B=%d outside (0, %d]", B, M->max_B);
   RV_CHECK_ARG(ws_bytes >= M->ws_bytes(B), "workspace %zu < %zu bytes", ws_bytes, M->ws_bytes(B));
   RV_CHECK_ARG(!cand || (cand_n && cand_cap > 0), "candidate buffers incomplete");
@@ -874,6 +898,15 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   M->trace.clear();
   M->launches.clear();
   M->fused.clear();
+  M->li_base = part == 2 ? M->n_part1 : 0;
+  // fused C2f chains (c2f.hip) unless a raw parity forward keeps every
+  // activation (RV_YOLO_OPT_RAW_UNFUSED) or RV_FUSE_C2F=0
+  static const bool c2f_env = !getenv("RV_FUSE_C2F") || atoi(getenv("RV_FUSE_C2F")) != 0;
+  const bool fuse_c2f = c2f_env && !f8 && M->fuse_c2f && !(raw_out && M->raw_unfused);
+  const int cat14 = v.h12 + v.c3, cat11 = v.c5 + v.c4, cat20 = v.h18 + v.c5,
+            cat17 = v.h15 + v.h12;
+  int st;
+  if (part != 2) {
   // backbone
   const ConvSpec& c0 = M->def.convs[0];
   // conv0 + model.1 fused (the P1 map stays in LDS) unless the caller asked
@@ -883,7 +916,6 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   const int i1 = M->def.find("model.1");
   const bool fuse_stem =
       stem_env && !f8 && !(raw_out && M->raw_unfused) && c0.cout == 16 && v.c2 == 32 && i1 >= 0;
-  int st;
   // the fused stem also runs model.2.cv1 (32 -> 32 1x1) from its registers
   // into the model.2 concat buffer when the shapes allow
   const int i2cv1 = M->def.find("model.2.cv1");
@@ -915,15 +947,9 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
     if (st) return st;
     E.conv("model.1", View{M->X0, v.c1, 0}, 1, View{M->X1, v.c2, 0});
   }
-  // fused C2f chains (c2f.hip) unless a raw parity forward keeps every
-  // activation (RV_YOLO_OPT_RAW_UNFUSED) or RV_FUSE_C2F=0
-  static const bool c2f_env = !getenv("RV_FUSE_C2F") || atoi(getenv("RV_FUSE_C2F")) != 0;
-  const bool fuse_c2f = c2f_env && !f8 && M->fuse_c2f && !(raw_out && M->raw_unfused);
   E.c2f("model.2", View{M->X1, v.c2, 0}, 2, M->C2, v.c2, v.nb, true, View{M->X2, v.c2, 0}, 0,
         View{-1, 0, 0}, 0, fuse_c2f, stem_cv1);
   E.conv("model.3", View{M->X2, v.c2, 0}, 2, View{M->X3, v.c3, 0});
-  const int cat14 = v.h12 + v.c3, cat11 = v.c5 + v.c4, cat20 = v.h18 + v.c5,
-            cat17 = v.h15 + v.h12;
   E.c2f("model.4", View{M->X3, v.c3, 0}, 3, M->C4, v.c3, v.nm, true,
         View{M->CAT14, cat14, v.h12}, 0, View{-1, 0, 0}, 0, fuse_c2f);
   E.conv("model.5", View{M->CAT14, cat14, v.h12}, 3, View{M->X5, v.c4, 0});
@@ -943,6 +969,12 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
   // head
   E.c2f("model.12", View{M->CAT11, cat11, 0}, 4, M->C12, v.h12, v.nb, false,
         View{M->CAT17, cat17, v.h15}, 0, View{M->CAT14, cat14, 0}, 1);
+  E.c2f("model.15", View{M->CAT14, cat14, 0}, 3, M->C15, v.h15, v.nb, false,
+        View{M->X15, v.h15, 0}, 0, View{-1, 0, 0}, 0, fuse_c2f);
+  if (E.status) return E.status;
+  M->n_part1 = (int)M->launches.size();
+  if (part == 1) return RV_OK;
+  }  // part != 2
   // Detect head of level i: box (cv2) and class (cv3) branches, one grouped
   // launch per stage; the last 1x1 stage runs inside the decode kernel
   // (RV_FUSE_HEAD=0: separate launches and f32 logits in HBM).  The P3 and
@@ -994,8 +1026,6 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
     if (!r && e) E.status = e;
     return r ? r : e;
   };
-  E.c2f("model.15", View{M->CAT14, cat14, 0}, 3, M->C15, v.h15, v.nb, false,
-        View{M->X15, v.h15, 0}, 0, View{-1, 0, 0}, 0, fuse_c2f);
   if (E.status || forked_head(0)) return E.status;
   E.conv("model.16", View{M->X15, v.h15, 0}, 3, View{M->CAT17, cat17, 0});
   E.c2f("model.18", View{M->CAT17, cat17, 0}, 4, M->C18, v.h18, v.nb, false,

@@ -91,6 +91,8 @@ _SIGS = {
     "rv_yolo_num_anchors": (c_int, [c_void_p]),
     "rv_yolo_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_float,
                                 c_void_p, c_int, c_void_p, c_void_p]),
+    "rv_yolo_forward_part": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p,
+                                     c_float, c_void_p, c_int, c_void_p, c_void_p, c_int]),
     "rv_yolo_num_buffers": (c_int, [c_void_p]),
     "rv_yolo_buffer_info": (c_int, [c_void_p, c_int, c_int, POINTER(c_int), POINTER(c_size_t)]),
     "rv_yolo_trace": (c_int, [c_void_p, c_void_p, c_int]),

@@ -216,18 +216,20 @@ class YoloEngine:
         B = frames.shape[0]
         return kernels.letterbox(frames, self.geo, out=self.lb[slot][:B])
 
-    def forward_raw(self, lb: torch.Tensor, raw: Optional[torch.Tensor] = None,
-                    candidates: bool = True, slot: int = 0, lane: int = 0):
+    def forward_raw(self, lb: Optional[torch.Tensor], raw: Optional[torch.Tensor] = None,
+                    candidates: bool = True, slot: int = 0, lane: int = 0, part: int = 0,
+                    batch: Optional[int] = None):
         """YOLOv8 forward + decode in forward context `lane`; candidates go to
-        candidate slot `slot`."""
-        B = lb.shape[0]
+        candidate slot `slot`.  part 1 / 2: the two halves of the forward
+        (rv_yolo_forward_part; part 2 takes no letterbox, `batch` gives B)."""
+        B = lb.shape[0] if lb is not None else int(batch)
         if B > self.max_batch:
             raise ValueError(f"batch {B} > max_batch {self.max_batch}")
-        lb = lb.contiguous()
-        call("rv_yolo_forward", self._hs[lane], ptr(lb), B, ptr(self.wss[lane]), self.ws_bytes,
-             ptr(raw),
-             self.conf, ptr(self.cand[slot]) if candidates else None, self.cap,
-             ptr(self.seg_n[slot]) if candidates else None, stream_ptr())
+        if lb is not None:
+            lb = lb.contiguous()
+        call("rv_yolo_forward_part", self._hs[lane], ptr(lb), B, ptr(self.wss[lane]),
+             self.ws_bytes, ptr(raw), self.conf, ptr(self.cand[slot]) if candidates else None,
+             self.cap, ptr(self.seg_n[slot]) if candidates else None, stream_ptr(), int(part))
         self._nseg_cur = self.nseg
         return raw
 

@@ -75,10 +75,12 @@ class RoadVisionEngine:
         proc = self.pipeline(frames)
         return proc, self.detector.letterbox(proc, lb_slot)
 
-    def yolo_stage(self, lb: torch.Tensor, slot: int = 0, lane: int = 0) -> None:
+    def yolo_stage(self, lb: Optional[torch.Tensor], slot: int = 0, lane: int = 0,
+                   part: int = 0) -> None:
         """YOLOv8 forward + decode in forward context `lane`; NMS candidates
-        land in candidate slot `slot`."""
-        self.detector.forward_raw(lb, slot=slot, lane=lane)
+        land in candidate slot `slot`.  part 1 / 2: the two halves of the
+        forward (YoloEngine.forward_raw)."""
+        self.detector.forward_raw(lb, slot=slot, lane=lane, part=part, batch=self.S)
 
     def detect_stage(self, frames: torch.Tensor, slot: int = 0) -> torch.Tensor:
         proc, lb = self.preprocess_stage(frames)
@@ -215,8 +217,8 @@ class OverlappedSteps:
             return {"record": o["record"]}
         if chunk is None:
             chunk = int(os.environ.get("RV_GRAPH_CHUNK", "8"))
-        self.staged = L > 1
-        if L > 1:
+        self.staged = L > 1 and depth != 4
+        if self.staged:
             # Per-stage graphs chained by events at replay time (run()): a
             # forward captured on a side stream of a multi-stream capture
             # crashes hipStreamEndCapture on ROCm 7.2 (tools/probe_lanes.py),
@@ -270,6 +272,9 @@ class OverlappedSteps:
                     self.graphs.append(g)
             return
         lbs = {}
+        if depth == 4:
+            self._capture_depth4(frames, track, procs, lbs, chunk, ctx, capture)
+            return
         # steps per captured graph (`chunk`, RV_GRAPH_CHUNK): consecutive
         # pipeline stages j are captured into one graph, so the device never
         # idles between graph replays inside a chunk; 0 = all K+2 stages in
@@ -296,6 +301,69 @@ class OverlappedSteps:
                     cur.wait_stream(side_t)
                     if j >= 1:
                         out["proc"] = procs.pop(j - 1)
+                        self.outs.append(out)
+            if capture:
+                self.graphs.append(g)
+
+    def _capture_depth4(self, frames, track, procs, lbs, chunk, ctx, capture):
+        """depth=4 with two forward lanes: the forward is split in two
+        (rv_yolo_forward_part) and stage j runs
+            P(j+1) || Y1(j) || Y2(j-1) || T(j-2)
+        -- the bandwidth-heavy first half of step j's forward beside the
+        latency-bound second half of step j-1's (each step's forward uses
+        lane j % 2: its own workspace), the preprocess of step j+1 and the
+        NMS + SORT of step j-2.  Y2 runs on the capture stream (it forks the
+        Detect heads); Y1, P and T on side streams."""
+        eng = self.eng
+        K = len(frames)
+        if eng.detector.lanes != 2:
+            raise ValueError("depth 4 needs RoadVisionEngine(lanes=2)")
+        dev = eng.device
+        side_p, side_t, side_y = (torch.cuda.Stream(dev) for _ in range(3))
+        slots = eng.detector.slots
+        js = list(range(-1, K + 2))
+        size = len(js) if chunk <= 0 else chunk
+        for c0 in range(0, len(js), size):
+            g = torch.cuda.CUDAGraph() if capture else None
+            with ctx(g):
+                for j in js[c0:c0 + size]:
+                    cur = torch.cuda.current_stream()
+                    for x in (side_p, side_t, side_y):
+                        x.wait_stream(cur)
+                    res = {}
+
+                    def p_(j=j):  # P(j+1) into letterbox slot (j+1) % slots
+                        if 0 <= j + 1 < K:
+                            with torch.cuda.stream(side_p):
+                                procs[j + 1], lbs[j + 1] = eng.preprocess_stage(
+                                    frames[j + 1], (j + 1) % slots)
+
+                    def t_(j=j):  # T(j-2) from candidate slot (j-2) % slots
+                        if 0 <= j - 2 < K:
+                            with torch.cuda.stream(side_t):
+                                res["out"] = track(j - 2)
+
+                    def y1_(j=j):  # Y1(j) on lane j % 2
+                        if 0 <= j < K:
+                            with torch.cuda.stream(side_y):
+                                eng.yolo_stage(lbs.pop(j), j % slots, j % 2, part=1)
+
+                    def y2_(j=j):  # Y2(j-1): candidates into slot (j-1) % slots
+                        if 0 <= j - 1 < K:
+                            eng.yolo_stage(None, (j - 1) % slots, (j - 1) % 2, part=2)
+                    # capture order = the graph executor's launch order, which
+                    # decides which HW queue a branch lands on and what it
+                    # queues behind: Y2, P, Y1, T measured best (tools: the
+                    # DESIGN.md schedule table; Y1 before P costs 10 %)
+                    y2_()
+                    p_()
+                    y1_()
+                    t_()
+                    out = res.get("out")
+                    for x in (side_p, side_t, side_y):
+                        cur.wait_stream(x)
+                    if 0 <= j - 2 < K:
+                        out["proc"] = procs.pop(j - 2)
                         self.outs.append(out)
             if capture:
                 self.graphs.append(g)

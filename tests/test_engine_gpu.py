@@ -111,12 +111,13 @@ def test_results_record_matches_device_outputs(cuda):
 
 
 @pytest.mark.parametrize("depth,chunk,lanes", [(2, None, 1), (3, 1, 1), (3, 3, 1), (3, None, 1),
-                                               (3, 0, 1), (3, None, 2), (3, 3, 2), (3, 0, 3)])
+                                               (3, 0, 1), (3, None, 2), (3, 3, 2), (3, 0, 3),
+                                               (4, None, 2), (4, 3, 2), (4, 0, 2)])
 def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk, lanes):
     """bench.py's timed mode (engine.OverlappedSteps): the track stage of step
     k runs on a side stream beside the preprocess of step k+1, with `chunk`
     pipeline stages per captured graph (None = the default 8, 0 = one graph);
-    lanes >= 2: the dependency-graph schedule with that many concurrent YOLO
+    lanes >= 2 (depth 3): the dependency-graph schedule with that many concurrent YOLO
     forwards.  EVERY step's handed-back detections / track ids and proc
     frames, and the final SORT state, must equal those of plain sequential
     step() calls."""
@@ -154,11 +155,12 @@ def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk, lanes):
     ovl.close()
 
 
-@pytest.mark.parametrize("lanes", [1, 2])
-def test_bench_configuration_parity(cuda, lanes):
+@pytest.mark.parametrize("depth,lanes", [(4, 2), (3, 1)])
+def test_bench_configuration_parity(cuda, depth, lanes):
     """Exactly bench.py's timed configuration (S = 32 streams of 1080p,
-    autotuned conv kernels, OverlappedSteps(depth=3, chunk=8), hand-back
-    into per-step host records), checked against the oracle on every step:
+    autotuned conv kernels, OverlappedSteps(depth=4, chunk=8) on two forward
+    lanes -- and the depth-3 one-lane pipeline --, hand-back into per-step
+    host records), checked against the oracle on every step:
     proc bit-exact on a sample of streams, NMS exact on the GPU's raw
     prediction for all 32 streams, SORT ids / distances exact for all 32
     streams, and no stream ever exceeds tmax."""
@@ -176,7 +178,7 @@ def test_bench_configuration_parity(cuda, lanes):
     eng.autotune(frames[0], reps=1)
     assert len(eng.detector.tuned_configs()) > 0
     run = OverlappedSteps(eng, [frames[WARM + k] for k in range(K)],
-                          [ts[WARM + k] for k in range(K)], depth=3, chunk=8)
+                          [ts[WARM + k] for k in range(K)], depth=depth, chunk=8)
     run.run()
     torch.cuda.synchronize()
     for k, o in enumerate(run.outs):
