@@ -69,7 +69,7 @@ def parse_args(argv=None):
     ap.add_argument("--tune-save", default=None, help="write the autotuned conv configs (JSON)")
     ap.add_argument("--tune-load", default=None,
                     help="load conv configs saved by --tune-save instead of autotuning")
-    ap.add_argument("--conv-timing", choices=["overlap", "eager", "none"], default="overlap",
+    ap.add_argument("--conv-timing", choices=["both", "overlap", "eager", "none"], default="both",
                     help="per-launch conv timing after the timed region: HIP events around "
                          "every conv launch while the timed region's multi-stream schedule runs "
                          "eagerly (overlap: same concurrency as the graphs), a plain sequential "
@@ -188,84 +188,102 @@ def rank_job(job, device) -> dict:
     return timed_job(job.run, job.sync, job.units, device)
 
 
-def conv_roofline(job, mode: str) -> dict:
-    """Per-launch conv timing with HIP events recorded on the launch stream
-    around every conv launch of K forwards.  Mode "overlap": the timed
-    region's own multi-stream schedule (OverlappedSteps: Y(k) beside P(k+1)
-    and T(k-1)) run eagerly, so every conv launch sees the concurrency it
-    sees inside the timed graphs (HIP events recorded inside captured graphs
-    read zero elapsed time on ROCm 7.2, so the graphs themselves cannot be
-    timed this way; the rocprofv3 trace of the timed region,
-    tools/trace_window.py, is the cross-check).  Mode "eager": one step at a
-    time.  achieved = algorithmic bytes (or FLOPs) of the conv family per
-    step / its measured time per step."""
+def _conv_pass(job, mode: str, tags):
+    """One profiled pass over the K steps: HIP events around every conv
+    launch of lane 0's forwards (rv_yolo_profile), bracketed by trace
+    markers `tags` so tools/trace_window.py can cut the same window out of
+    a rocprofv3 trace.  Returns (ms per forward, FLOPs, bytes, launches)."""
     from rvs_amd import _lib
     from rvs_amd.engine import OverlappedSteps
     eng, K, Wm = job.eng, job.K, job.Wm
     lib = _lib.load()
     h = eng.detector._h
     _lib.check(lib.rv_yolo_profile(h, K), "rv_yolo_profile")
-    used = mode
-    pipelined = job.runner is not None
-    job.runner = None  # release the timed graphs (and their memory pool) first
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()
+    st = _lib.stream_ptr()
+    _lib.call("rv_trace_marker", tags[0], st)
     prof = None
-    if mode == "overlap" and pipelined:
+    if mode == "overlap":
         prof = OverlappedSteps(eng, [job.frames[Wm + k] for k in range(K)],
                                [job.ts[Wm + k] for k in range(K)], depth=job.args.depth,
                                chunk=job.args.graph_chunk, capture=False)
-        torch.cuda.synchronize()
     else:
-        used = "eager"
         for k in range(K):
             eng.step(job.frames[Wm + k], job.ts[Wm + k])
-        torch.cuda.synchronize()
+    _lib.call("rv_trace_marker", tags[1], st)
+    torch.cuda.synchronize()
     n = lib.rv_yolo_num_convs(eng.variant)
-    ms = np.zeros(n, np.float64)
-    fl = np.zeros(n, np.float64)
+    ms, fl, by = np.zeros(n), np.zeros(n), np.zeros(n)
     cv = np.zeros(n, np.int32)
     nf = lib.rv_yolo_profile_read(h, ms.ctypes.data, fl.ctypes.data, cv.ctypes.data, n)
-    by = np.zeros(n, np.float64)
     lib.rv_yolo_profile_bytes(h, by.ctypes.data, n)
-    prof = None  # the graphs hold the events: destroy them before the events
+    prof = None  # noqa: F841 -- eager schedule objects before the events
     torch.cuda.synchronize()
     lib.rv_yolo_profile(h, 0)
     valid = cv >= 0
-    conv_ms = float(ms[valid].sum()) / max(nf, 1)
-    flop = float(fl[valid].sum())
-    byts = float(by[valid].sum())
-    if conv_ms <= 0.0:
-        return {"timing": used, "error": "no event timings"}
-    tflops = flop / (conv_ms * 1e-3) / 1e12
-    gbs = byts / (conv_ms * 1e-3) / 1e9
-    # which roofline binds the conv family: its algorithmic bytes at peak HBM
-    # vs its FLOPs at peak bf16 MFMA (small channel counts: bytes win)
-    hbm = byts / (PEAK_HBM * 1e9) >= flop / (PEAK_BF16 * 1e12)
+    return (float(ms[valid].sum()) / max(nf, 1), float(fl[valid].sum()), float(by[valid].sum()),
+            int(valid.sum()))
+
+
+def conv_roofline(job, mode: str) -> dict:
+    """Roofline of the conv family (every conv launch of a step:
+    conv_patch_kernel, conv1x1_direct_kernel, c2f_chain_kernel) from HIP
+    events recorded on the launch stream around every conv launch
+    (rv_yolo_profile; HIP events recorded inside captured graphs read zero
+    elapsed time on ROCm 7.2, so the timed graphs themselves cannot be timed
+    this way).  achieved = algorithmic bytes (or FLOPs) of the family per
+    step / its measured time per step.
+      "eager": one step at a time, each launch alone -- the kernels' own
+               speed (the headline `roofline`; rocprofv3 cross-check: the
+               trace window between the 5th and 6th rv_trace_marker);
+      "overlap": the timed region's multi-stream schedule run eagerly, so
+               each launch sees the concurrency it sees inside the timed
+               graphs (`in_pipeline`; window: markers 3 and 4).
+    "both" measures both."""
+    eng = job.eng
+    job.runner = None  # release the timed graphs (and their memory pool) first
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    res = {}
+    for m, tags in (("overlap", (3, 4)), ("eager", (5, 6))):
+        if mode in (m, "both"):
+            res[m] = _conv_pass(job, m, tags)
     traffic = None
     if os.path.exists(PMC_TRAFFIC):
         traffic = json.load(open(PMC_TRAFFIC)).get("conv_bytes_per_step")
-    return {
-        "kernel": "conv family: conv_patch_kernel + conv1x1_direct_kernel (all YOLOv8n conv "
-                  "launches of a step; HIP events on the launch stream)",
-        "timing": used + (" (the timed region's 3-stream schedule run eagerly: each conv "
-                          "launch timed under the same concurrency)" if used == "overlap" else
-                          " (one step at a time)"),
-        "bound": "hbm" if hbm else "mfma",
-        "achieved": round(gbs if hbm else tflops, 2),
-        "peak": PEAK_HBM if hbm else PEAK_BF16,
-        "unit": "GB/s" if hbm else "TFLOP/s",
-        "frac": round(gbs / PEAK_HBM if hbm else tflops / PEAK_BF16, 5),
-        "traffic": traffic,
-        "traffic_unit": "bytes per step (all conv launches; rocprofv3 PMC 2 x FETCH_SIZE + "
-                        "WRITE_SIZE, separate passes; profiles/r02/pmc_traffic.json)",
-        "algorithmic_bytes_per_step": round(byts),
-        "algorithmic_gflop_per_step": round(flop / 1e9, 2),
-        "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / PEAK_BF16, 5),
-        "hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / PEAK_HBM, 5),
-        "launches_per_step": int(valid.sum()),
-        "conv_ms_per_step": round(conv_ms, 4),
-    }
+
+    def view(conv_ms, flop, byts, nl):
+        tflops = flop / (conv_ms * 1e-3) / 1e12
+        gbs = byts / (conv_ms * 1e-3) / 1e9
+        # which roofline binds the conv family: its algorithmic bytes at peak
+        # HBM vs its FLOPs at peak bf16 MFMA (small channel counts: bytes win)
+        hbm = byts / (PEAK_HBM * 1e9) >= flop / (PEAK_BF16 * 1e12)
+        return {"bound": "hbm" if hbm else "mfma",
+                "achieved": round(gbs if hbm else tflops, 2),
+                "peak": PEAK_HBM if hbm else PEAK_BF16,
+                "unit": "GB/s" if hbm else "TFLOP/s",
+                "frac": round(gbs / PEAK_HBM if hbm else tflops / PEAK_BF16, 5),
+                "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / PEAK_BF16, 5),
+                "hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / PEAK_HBM, 5),
+                "launches_per_step": nl, "conv_ms_per_step": round(conv_ms, 4),
+                "algorithmic_bytes_per_step": round(byts),
+                "algorithmic_gflop_per_step": round(flop / 1e9, 2)}
+    if not res or any(v[0] <= 0 for v in res.values()):
+        return {"error": "no event timings"}
+    main = "eager" if "eager" in res else "overlap"
+    out = {"kernel": "conv family: conv_patch_kernel + conv1x1_direct_kernel + c2f_chain_kernel "
+                     "(all YOLOv8n conv launches of a step; HIP events on the launch stream)",
+           "timing": main + (" (one step at a time: each launch alone)" if main == "eager" else
+                             " (the timed region's schedule run eagerly)")}
+    out.update(view(*res[main]))
+    out["traffic"] = traffic
+    out["traffic_unit"] = ("bytes per step (all conv launches; rocprofv3 PMC 2 x FETCH_SIZE + "
+                           "WRITE_SIZE, separate passes over one eager step; "
+                           "profiles/r02/pmc_traffic.json)")
+    if main == "eager" and "overlap" in res:
+        out["in_pipeline"] = dict(view(*res["overlap"]), timing=(
+            "the timed region's schedule run eagerly: each conv launch timed under the "
+            "concurrency it has inside the timed graphs"))
+    return out
 
 
 def host_cpu_model() -> str:

@@ -9,11 +9,16 @@ STEPS=${STEPS:-60}
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/raw" -o trace -- \
   python3 bench.py --tune-load "$TUNE" --warmup 1 --steps "$STEPS" --no-cpu-baseline \
-  --conv-timing none ${BENCH_ARGS:-} > "$OUT/bench_profiled.json" 2> "$OUT/bench_profiled.err" || exit $?
+  --conv-timing ${CONV_TIMING:-none} ${BENCH_ARGS:-} > "$OUT/bench_profiled.json" \
+  2> "$OUT/bench_profiled.err" || exit $?
 KT=$(find "$OUT/raw" -name "*kernel_trace.csv" | head -1)
 ST=$(find "$OUT/raw" -name "*kernel_stats.csv" | head -1)
 cp "$ST" "$OUT/rocprof_kernel_stats_whole_run.csv"
 python3 tools/trace_window.py "$KT" "$STEPS" "$OUT/timed" || exit $?
 python3 tools/stream_busy.py "$KT" "$STEPS" > "$OUT/timed_streams.txt" || exit $?
+if [ "${CONV_TIMING:-none}" = both ]; then  # the conv profiling passes' windows
+  python3 tools/trace_window.py "$KT" "$STEPS" "$OUT/convpass_pipeline" 1 > /dev/null || exit $?
+  python3 tools/trace_window.py "$KT" "$STEPS" "$OUT/convpass_eager" 2 > /dev/null || exit $?
+fi
 gzip -c "$KT" > "$OUT/kernel_trace.csv.gz"
 rm -rf "$OUT/raw"

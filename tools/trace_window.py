@@ -3,7 +3,10 @@ trace: keeps the dispatches between the two rv_trace_marker kernels bench.py
 launches right before and right after its timed region (tags 1 and 2), so
 warm-up, autotuning, capture and the CPU baseline are excluded.
 
-usage: python tools/trace_window.py kernel_trace.csv STEPS OUT_PREFIX
+usage: python tools/trace_window.py kernel_trace.csv STEPS OUT_PREFIX [PAIR]
+PAIR (default 0) picks the window between marker dispatches 2*PAIR and
+2*PAIR+1: 0 = the timed region, 1 = bench.py's in-pipeline conv profiling
+pass, 2 = its eager conv profiling pass (--conv-timing both).
 writes OUT_PREFIX_kernel_stats.csv (rocprofv3 --stats columns) and
 OUT_PREFIX_summary.txt (per-step time of each kernel family, conv family
 included, and the window's wall time)."""
@@ -11,7 +14,7 @@ import csv
 import sys
 from collections import defaultdict
 
-CONV = ("conv_patch_kernel", "conv1x1_direct_kernel")
+CONV = ("conv_patch_kernel", "conv1x1_direct_kernel", "c2f_chain_kernel")
 
 
 def family(name: str) -> str:
@@ -21,14 +24,15 @@ def family(name: str) -> str:
 
 def main():
     path, steps, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
+    pair = int(sys.argv[4]) if len(sys.argv) > 4 else 0
     rows = []
     for r in csv.DictReader(open(path)):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     marks = [i for i, r in enumerate(rows) if "rv_trace_marker_kernel" in r[2]]
-    if len(marks) < 2:
-        sys.exit(f"need 2 rv_trace_marker dispatches, found {len(marks)}")
-    a, b = marks[0], marks[1]
+    if len(marks) < 2 * pair + 2:
+        sys.exit(f"need {2 * pair + 2} rv_trace_marker dispatches, found {len(marks)}")
+    a, b = marks[2 * pair], marks[2 * pair + 1]
     win = rows[a + 1:b]
     t0, t1 = rows[a][1], rows[b][0]
     agg = defaultdict(list)
