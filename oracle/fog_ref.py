@@ -60,10 +60,12 @@ def draw(rng, h, w, level="medium", mor=None, scale_ratio=0.18, n_oct=2, rain=Fa
     rng.rand()  # contrast drop
     tint = (1.0 + rng.uniform(-0.015, 0.02, size=3)).astype(F)
     gamma = 1.0 + rng.uniform(-0.04, 0.05) if rng.rand() < 0.35 else 1.0
-    rng.rand()  # sensor-noise coin
+    noise = rng.rand() < 0.3  # sensor-noise coin (fog.py:293-295)
+    if noise:  # not applied, but its normals advance the stream
+        rng.normal(0, 0.0035, size=(h, w, 3))
     seed = rng.randint(1 << 24) if rain else 0
     return dict(beta=F(beta), a_rgb=a_rgb.astype(F), a_scale=F(a_scale), tint=tint,
-                gamma=F(gamma), rain_seed=int(seed), grids=grids)
+                gamma=F(gamma), rain_seed=int(seed), grids=grids, sensor_noise=bool(noise))
 
 
 def _lowbias32(x):

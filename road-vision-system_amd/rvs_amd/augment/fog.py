@@ -165,7 +165,9 @@ class FogSynthesizer:
         gamma = 1.0
         if rng.rand() < 0.35:  # fog.py:290-292
             gamma = 1.0 + rng.uniform(-0.04, 0.05)
-        rng.rand()  # sensor-noise coin (fog.py:293); the normals are not drawn
+        if rng.rand() < 0.3:  # sensor noise (fog.py:293-295): not applied, but its
+            rng.normal(0, 0.0035, size=(h, w, 3))  # normals advance the stream
+            # exactly as the reference's do, so later frames' draws match
         rain_seed = rng.randint(1 << 24) if self.rain_p > 0 else 0
         params = np.zeros(NPARAM, _F)
         params[:10] = [base_beta, a_rgb[0], a_rgb[1], a_rgb[2], scale, tint[0], tint[1],

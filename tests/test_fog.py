@@ -35,6 +35,25 @@ def test_host_draw_matches_oracle(kw, hw):
         np.testing.assert_array_equal(g, np.concatenate([x.ravel() for x in r["grids"]]))
 
 
+def test_multi_frame_draws_follow_reference_stream():
+    """A seeded sequence keeps the reference's RNG stream across frames: when
+    the sensor-noise coin fires (fog.py:293-295) the H x W x 3 normals are
+    drawn (and discarded), so every later frame's beta / airlight / tint /
+    gamma equal the reference's.  Eight 37 x 91 frames; the coin must fire
+    at least once for the check to mean anything."""
+    syn = _synth(seed=11, rain_p=0.01)
+    rng = np.random.RandomState(11)
+    fired = 0
+    for _ in range(8):
+        p, g = syn.draw(37, 91)
+        r = fog_ref.draw(rng, 37, 91, rain=True)
+        fired += r["sensor_noise"]
+        assert p[0] == r["beta"] and p[4] == r["a_scale"] and p[8] == r["gamma"]
+        np.testing.assert_array_equal(p[5:8], r["tint"])
+        assert int(p[9]) == r["rain_seed"]
+    assert fired > 0
+
+
 def test_scene_constants_follow_depth_proxy():
     from rvs_amd.augment import fog_scene, perlin_octaves
     h, w = 384, 640
