@@ -22,6 +22,7 @@ namespace rv {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
 
 typedef __attribute__((ext_vector_type(2))) float f32x2v;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
@@ -562,7 +563,25 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
     for (int kx = 0; kx < K; ++kx) {
       const int sc = patch_scol<S>(pc + kx, g.PW);
       const int lq = F8 ? quad >> 1 : quad;
-      boff[n][kx] = (pr * g.PW + sc) * 64 + ((lq ^ swzq<F8>(sc)) << 4) + (F8 ? (quad & 1) * 8 : 0);
+      if constexpr (F8 && K == 3)  // tap-pair path: pixel slot base | swizzle (low bits)
+        boff[n][kx] = (pr * g.PW + sc) * 64 + swzq<true>(sc);
+      else
+        boff[n][kx] = (pr * g.PW + sc) * 64 + ((lq ^ swzq<F8>(sc)) << 4) + (F8 ? (quad & 1) * 8 : 0);
+    }
+  }
+  // fp8 3x3 convs run v_mfma_scale_f32_16x16x128_f8f6f4 (unit scales) on tap
+  // pairs: k-slots 32q .. 32q+31 of lane quad q = channels 32 (q & 1) ..
+  // +31 of tap t + (q >> 1) -- two 16-B quarters of that tap's 64-B slot.
+  // aoff: this lane's two weight-quarter offsets within a (row, tap) slot
+  // pair, per m (row = m*16 + col; the swizzle of the row picks the order)
+  int aoff[F8 && K == 3 ? MR : 1][2];
+  if constexpr (F8 && K == 3) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      const int row = m * 16 + col, sw = swzq<true>(row);
+      const int base = (row * T2 + (quad >> 1)) * 64;
+      aoff[m][0] = base + (((2 * (quad & 1)) ^ sw) << 4);
+      aoff[m][1] = base + (((2 * (quad & 1) + 1) ^ sw) << 4);
     }
   }
   f32x4 bias[MR], dq[MR];
@@ -646,6 +665,41 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
       if (c >= nch) break;
       const uint8_t* P = stages + buf * stage_bytes + gi * chunk_bytes;
       const uint8_t* Wl = RESW ? smem + c * W_BYTES : P + g.p_bytes;
+      if constexpr (F8 && K == 3) {
+        const int rowb = g.PW * PB;
+#pragma unroll
+        for (int t = 0; t < 9; t += 2) {
+          const bool odd = t + 1 >= 9;  // the last tap pairs with zeros
+          const int ky0 = t / 3, kx0 = t % 3;
+          const int ky1 = odd ? ky0 : (t + 1) / 3, kx1 = odd ? kx0 : (t + 1) % 3;
+          const bool hi = (quad >> 1) != 0;
+          i32x8 A[MR], Bv[NR];
+#pragma unroll
+          for (int m = 0; m < MR; ++m) {
+            const uint4 lo = *(const uint4*)(Wl + aoff[m][0] + t * 64);
+            const uint4 up = *(const uint4*)(Wl + aoff[m][1] + t * 64);
+            A[m] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w,
+                         (int)up.x, (int)up.y, (int)up.z, (int)up.w};
+            if (odd && hi) A[m] = i32x8{0, 0, 0, 0, 0, 0, 0, 0};
+          }
+#pragma unroll
+          for (int n = 0; n < NR; ++n) {
+            const int v = hi ? boff[n][kx1] + ky1 * rowb : boff[n][kx0] + ky0 * rowb;
+            const int sw = v & 3, base = v & ~63;
+            const uint4 lo = *(const uint4*)(P + base + (((2 * (quad & 1)) ^ sw) << 4));
+            const uint4 up = *(const uint4*)(P + base + (((2 * (quad & 1) + 1) ^ sw) << 4));
+            Bv[n] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w,
+                          (int)up.x, (int)up.y, (int)up.z, (int)up.w};
+          }
+#pragma unroll
+          for (int m = 0; m < MR; ++m)
+#pragma unroll
+            for (int n = 0; n < NR; ++n)
+              acc[m][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                  A[m], Bv[n], acc[m][n], 0, 0, 0, 127, 0, 127);
+        }
+        continue;
+      }
       // kernel rows are not unrolled for the largest tiles: the fragments of
       // one row (3 taps) in flight keep them under the register file
 #pragma unroll(F8 || MR * NR >= 16 ? 1 : K)
@@ -1029,13 +1083,15 @@ constexpr bool patch_spills(int MR, int NR, int K, int S, bool RESW) {
 }
 
 // fp8 instantiations: MR, NR in {1, 2, 4}; the 3x3 ones that exceed the
-// register file (4x4, and 1x2 stride 2 with staged weights) are not built
+// register file (4x4, 2x4 stride 1, 1x2 stride 2 with staged weights) are
+// not built
 template <int MR, int NR>
 constexpr bool tile8_built() {
   return (MR == 1 || MR == 2 || MR == 4) && (NR == 1 || NR == 2 || NR == 4);
 }
 constexpr bool patch_spills8(int MR, int NR, int K, int S, bool RESW) {
-  return K == 3 && (MR * NR >= 16 || (S == 2 && !RESW && MR == 1 && NR == 2));
+  return K == 3 && (MR * NR >= 16 || (S == 1 && MR == 2 && NR == 4) ||
+                    (S == 2 && !RESW && MR == 1 && NR == 2));
 }
 
 template <int MR, int NR, bool RESW>
