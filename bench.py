@@ -198,7 +198,9 @@ def _conv_pass(job, mode: str, tags):
     eng, K, Wm = job.eng, job.K, job.Wm
     lib = _lib.load()
     h = eng.detector._h
-    _lib.check(lib.rv_yolo_profile(h, K), "rv_yolo_profile")
+    # eager: each conv launched 5x back to back between its events, so an
+    # event pair times kernels, not the dispatch gap in front of one kernel
+    _lib.check(lib.rv_yolo_profile_reps(h, K, 5 if mode == "eager" else 1), "rv_yolo_profile")
     st = _lib.stream_ptr()
     _lib.call("rv_trace_marker", tags[0], st)
     prof = None
@@ -232,9 +234,10 @@ def conv_roofline(job, mode: str) -> dict:
     elapsed time on ROCm 7.2, so the timed graphs themselves cannot be timed
     this way).  achieved = algorithmic bytes (or FLOPs) of the family per
     step / its measured time per step.
-      "eager": one step at a time, each launch alone -- the kernels' own
-               speed (the headline `roofline`; rocprofv3 cross-check: the
-               trace window between the 5th and 6th rv_trace_marker);
+      "eager": one step at a time, each launch alone, five times back to
+               back between its events -- the kernels' own speed (the
+               headline `roofline`; rocprofv3 cross-check: the trace window
+               between the 5th and 6th rv_trace_marker);
       "overlap": the timed region's multi-stream schedule run eagerly, so
                each launch sees the concurrency it sees inside the timed
                graphs (`in_pipeline`; window: markers 3 and 4).

@@ -237,6 +237,10 @@ int rv_yolo_trace(void* handle, int* recs, int max_recs);
  * per conv launch index, the summed ms over the recorded forwards, the
  * algorithmic FLOPs of one launch (2*M*N*K) and the conv index. */
 int rv_yolo_profile(void* handle, int max_forwards);
+/* The same with every profiled conv launched `reps` times back to back
+ * between its event pair (same inputs and output); profile_read then
+ * reports the time of ONE launch, free of the per-event dispatch gap. */
+int rv_yolo_profile_reps(void* handle, int max_forwards, int reps);
 int rv_yolo_profile_read(void* handle, double* ms, double* flops, int* conv, int n);
 /* Algorithmic HBM bytes of one launch per conv launch index (inputs read
  * once, outputs written, residual, weights); returns the entries written. */

@@ -224,6 +224,7 @@ struct TraceRec {
 struct Profile {
   bool on = false;
   int cap_fwd = 0, n_fwd = 0, per_fwd = 0;
+  int reps = 1;  // launches of each conv between its event pair (rv_yolo_profile_reps)
   std::vector<hipEvent_t> ev;     // [cap_fwd][per_fwd][2]
   std::vector<double> flops;      // per conv launch index (algorithmic, 2*M*N*K)
   std::vector<double> bytes;      // per conv launch index (algorithmic HBM bytes, launch_bytes)
@@ -495,14 +496,20 @@ struct Exec {
         rec ? hip_check(hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + li_) * 2], s),
                         "profile hipEventRecord")
             : RV_OK;
-    if (a.fused > 0) {
-      const Model::FusedC2f& f = M->fused[a.fused - 1];
-      status = launch_c2f_chain(f.a, f.C, f.N, f.shortcut, s);
-    } else if (li_ < (int)M->tuned.size() && M->tuned[li_].mr > 0 &&
-               conv_cfg_ok(a, M->tuned[li_])) {
-      status = launch_conv_cfg(a, M->tuned[li_], s);
-    } else {
-      status = launch_conv(a, s);
+    // profiled forwards may launch each conv `reps` times back to back
+    // between its events (the same inputs, the same output): the event pair
+    // then times reps kernels, not reps dispatch latencies
+    const int nrep = rec ? P.reps : 1;
+    for (int r = 0; r < nrep && !status; ++r) {
+      if (a.fused > 0) {
+        const Model::FusedC2f& f = M->fused[a.fused - 1];
+        status = launch_c2f_chain(f.a, f.C, f.N, f.shortcut, s);
+      } else if (li_ < (int)M->tuned.size() && M->tuned[li_].mr > 0 &&
+                 conv_cfg_ok(a, M->tuned[li_])) {
+        status = launch_conv_cfg(a, M->tuned[li_], s);
+      } else {
+        status = launch_conv(a, s);
+      }
     }
     if (!status) status = ev0;
     if (rec && !status)
@@ -1095,10 +1102,11 @@ extern "C" int rv_yolo_trace(void* h, int* recs, int max_recs) {
 }
 
 // ---- live conv timing ------------------------------------------------------
-extern "C" int rv_yolo_profile(void* h, int max_forwards) {
-  RV_CHECK_ARG(h && max_forwards >= 0, "bad args");
+extern "C" int rv_yolo_profile_reps(void* h, int max_forwards, int reps) {
+  RV_CHECK_ARG(h && max_forwards >= 0 && reps >= 1, "bad args");
   Model* M = (Model*)h;
   Profile& P = M->prof;
+  P.reps = reps;
   for (hipEvent_t e : P.ev) (void)hipEventDestroy(e);  // teardown
   P.ev.clear();
   P.on = max_forwards > 0;
@@ -1116,6 +1124,10 @@ extern "C" int rv_yolo_profile(void* h, int max_forwards) {
       return RV_EINVAL;
     }
   return RV_OK;
+}
+
+extern "C" int rv_yolo_profile(void* h, int max_forwards) {
+  return rv_yolo_profile_reps(h, max_forwards, 1);
 }
 
 // After the profiled forwards (synchronises): per conv launch index i,
@@ -1136,7 +1148,7 @@ extern "C" int rv_yolo_profile_read(void* h, double* ms, double* flops, int* con
           hipEventElapsedTime(&t, a, b) == hipSuccess)
         tot += t;
     }
-    ms[i] = tot;
+    ms[i] = tot / P.reps;
     flops[i] = P.flops[i];
     conv[i] = P.conv_of[i];
   }

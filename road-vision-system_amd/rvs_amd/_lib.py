@@ -97,6 +97,7 @@ _SIGS = {
     "rv_yolo_buffer_info": (c_int, [c_void_p, c_int, c_int, POINTER(c_int), POINTER(c_size_t)]),
     "rv_yolo_trace": (c_int, [c_void_p, c_void_p, c_int]),
     "rv_yolo_profile": (c_int, [c_void_p, c_int]),
+    "rv_yolo_profile_reps": (c_int, [c_void_p, c_int, c_int]),
     "rv_yolo_profile_read": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
     "rv_yolo_profile_bytes": (c_int, [c_void_p, c_void_p, c_int]),
     "rv_yolo_autotune": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_int, c_int,
