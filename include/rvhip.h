@@ -264,6 +264,10 @@ int rv_yolo_tuned_config(void* handle, int idx, int* cfg6);
  * autotune), so a run can skip the autotuner; an invalid entry falls back to
  * the default heuristic at launch. */
 int rv_yolo_set_tuned(void* handle, int n, int idx, const int* cfg6);
+/* The valid configurations of conv launch idx of the last whole forward
+ * (cfg6 entries as above, at most cap written); returns the count (0 for a
+ * fused C2f launch). */
+int rv_yolo_conv_candidates(void* handle, int idx, int* cfg6, int cap);
 
 /* --- Ultralytics non_max_suppression + scale_boxes + class filter
  * (yolo_ultralytics.py:28-53), one workgroup per image. */

@@ -1312,6 +1312,32 @@ extern "C" int rv_yolo_set_tuned(void* h, int n, int idx, const int* cfg6) {
   return RV_OK;
 }
 
+// The valid kernel configurations of conv launch idx of the last whole
+// forward (the autotuner's search space for it; fused C2f launches have
+// none): writes up to cap entries of cfg6 = {MR, NR, G, resw, persist, kind}
+// and returns the count.  A caller that times configurations in its own
+// schedule (bench.py's in-pipeline tuning) installs them with
+// rv_yolo_set_tuned.
+extern "C" int rv_yolo_conv_candidates(void* h, int idx, int* cfg6, int cap) {
+  RV_CHECK_ARG(h, "null handle");
+  Model* M = (Model*)h;
+  RV_CHECK_ARG(idx >= 0 && idx < (int)M->launches.size(),
+               "launch %d not in the last forward (%d launches)", idx, (int)M->launches.size());
+  const ConvArgs& a = M->launches[idx];
+  if (a.fused > 0) return 0;
+  std::vector<ConvCfg> c(512);
+  const int n = std::min(conv_candidates(a, c.data(), (int)c.size()), (int)c.size());
+  for (int i = 0; i < n && i < cap && cfg6; ++i) {
+    cfg6[6 * i] = c[i].mr;
+    cfg6[6 * i + 1] = c[i].nr;
+    cfg6[6 * i + 2] = c[i].G;
+    cfg6[6 * i + 3] = c[i].resw;
+    cfg6[6 * i + 4] = c[i].persist;
+    cfg6[6 * i + 5] = c[i].kind;
+  }
+  return n;
+}
+
 // Algorithmic HBM bytes of each conv launch of the profiled forwards (same
 // indexing as rv_yolo_profile_read); returns the number of entries written.
 extern "C" int rv_yolo_profile_bytes(void* h, double* bytes, int n) {

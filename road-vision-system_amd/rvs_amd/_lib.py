@@ -104,6 +104,7 @@ _SIGS = {
                                  POINTER(c_int), c_void_p]),
     "rv_yolo_tuned_config": (c_int, [c_void_p, c_int, POINTER(c_int)]),
     "rv_yolo_set_tuned": (c_int, [c_void_p, c_int, c_int, POINTER(c_int)]),
+    "rv_yolo_conv_candidates": (c_int, [c_void_p, c_int, c_void_p, c_int]),
     "rv_trace_marker": (c_int, [c_int, c_void_p]),
     "rv_nms_smem_bytes": (c_size_t, []),
     "rv_nms_postprocess": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int,
@@ -161,7 +162,7 @@ def check(status: int, what: str = "") -> None:
 
 _NOCHECK = {"rv_abi_version", "rv_cand_segments", "rv_yolo_cand_segments", "rv_clahe_median_fits", "rv_clahe_median_letterbox_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
             "rv_yolo_num_buffers", "rv_yolo_trace", "rv_yolo_profile_read", "rv_yolo_tuned_config",
-            "rv_yolo_profile_bytes", "rv_yolo_buffer_esize"}
+            "rv_yolo_profile_bytes", "rv_yolo_buffer_esize", "rv_yolo_conv_candidates"}
 
 
 def call(name: str, *args) -> int:

@@ -261,6 +261,17 @@ class YoloEngine:
             out.append(tuple(c))
         return out
 
+    def conv_candidates(self, idx: int):
+        """Valid (MR, NR, G, resw, persist, kind) configurations of conv
+        launch idx of the last whole forward of lane 0 ([] for a fused C2f
+        launch)."""
+        n = call("rv_yolo_conv_candidates", self._h, int(idx), None, 0)
+        if n < 0:
+            _lib.check(n, "rv_yolo_conv_candidates")
+        buf = (ctypes.c_int * (6 * max(n, 1)))()
+        call("rv_yolo_conv_candidates", self._h, int(idx), buf, n)
+        return [tuple(buf[6 * i:6 * i + 6]) for i in range(n)]
+
     def load_tuned(self, cfgs) -> None:
         """Install saved per-launch configurations (tuned_configs() of an
         earlier autotune of the same plan) instead of autotuning."""
