@@ -444,31 +444,51 @@ __global__ __launch_bounds__(256) void median_tile_kernel(const uint8_t* __restr
 // ---------------------------------------------------------------------------
 // 3x3 fast path: med3_kernel<CLAHE, LB>.
 // Block = 256 threads -> 128 x 32 output pixels of one frame.
-//  1. (CLAHE) the block's interpolation cells go to LDS as packed u32
+//  1. the (32+2) x (128+2) halo tile is loaded as 32 four-pixel groups per
+//     row (12 bytes, three dword loads) plus the two side pixels, all issued
+//     first so their latency overlaps step 2.
+//  2. (CLAHE) the block's interpolation cells go to LDS as packed u32
 //     entries: cell (cy, cx) = the 4 tile LUTs one pixel blends, so a pixel
-//     costs ONE ds_read_b32 for its l11|l12|l21|l22.
-//  2. the (32+2) x (128+8) halo tile is loaded in 4-pixel groups (12 bytes,
-//     three dword loads, all issued before any use), CLAHE'd in registers
-//     and stored to LDS as 3 dwords per group.
-//  3. each thread produces a 4 x 4 block of medians (4 px wide, 4 rows):
+//     costs ONE ds_read_b32 for its l11|l12|l21|l22.  The cell area is
+//     dynamic LDS sized by the host for the geometry (4 KB at 1080p/8x8).
+//  3. the groups are CLAHE'd in registers and stored to LDS as 3 dwords.
+//  4. each thread produces a 4 x 4 block of medians (4 px wide, 4 rows):
 //     it reads 6 tile rows x 20 bytes with dword loads, sorts every 3-row
 //     column once (min3/med3/max3) and combines 3 columns per output:
 //     med = med3(max3(lo), med3(mid), min3(hi))  -- exact for 9 samples.
-//  4. (LB) medians are also kept in LDS and the letterbox pixels whose
-//     bilinear support lies in this block are produced from them
+//  5. (LB) the medians overwrite the halo tile in LDS (after a barrier:
+//     every thread holds its 6 rows in registers) and the letterbox pixels
+//     whose bilinear support lies in this block are produced from them
 //     (cv2.resize INTER_LINEAR fixed point, lbgeo.h).  The host only picks
 //     LB when every letterbox pixel's support falls inside one block.
+// LDS: 14.1 KB tile + cells + 1.3 KB taps, so 5-6 blocks fit a CU.
 // ---------------------------------------------------------------------------
 constexpr int kM3W = 128, kM3H = 32;
-constexpr int kM3TW = kM3W + 8;         // tile px x0-4 .. x0+131
+constexpr int kM3TW = kM3W + 8;         // tile bytes cover px x0-4 .. x0+131 (x0-1 .. x0+128 used)
 constexpr int kM3TH = kM3H + 2;         // tile rows y0-1 .. y0+32
-constexpr int kM3Groups = kM3TW / 4;    // 34 four-pixel groups per row
-constexpr int kM3Stride = 416;          // tile row bytes (408 used)
-constexpr int kM3OStride = kM3W * 3 + 16;  // median tile row bytes (LB)
-constexpr int kCellMax = 16;            // packed LUT cells per block (16 KB)
-constexpr int kM3Iter = (kM3TH * kM3Groups + 255) / 256;  // 5
+constexpr int kM3Stride = 416;          // tile row bytes (408 used; median tile 384)
+constexpr int kCellMax = 16;            // packed LUT cells per block (<= 16 KB)
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// Two output channels of ycrcb_to_bgr at once.  lo4/hi4 are the channel
+// terms scaled by 4 ((4x) >> 16 == x >> 14, so each term is the high half);
+// one v_perm_b32 gathers both, v_pk_add_u16 adds the luma of each half
+// (|y + term| < 2^15, so the i16 view is exact) and v_sat_pk_u8_i16
+// saturates and packs: bytes {sat(ylo + lo), sat(yhi + hi)} in the low half.
+__device__ __forceinline__ uint32_t ycc_pair(int lo4, int hi4, uint32_t ylo, uint32_t yhi) {
+  const uint32_t t = __builtin_amdgcn_perm((uint32_t)hi4, (uint32_t)lo4, 0x07060302u);
+  const u16x2 s = __builtin_bit_cast(u16x2, t) + __builtin_bit_cast(u16x2, ylo | (yhi << 16));
+  uint32_t r;
+  asm("v_sat_pk_u8_i16 %0, %1" : "=v"(r) : "v"(__builtin_bit_cast(uint32_t, s)));
+  return r;
+}
+
+// low 16 bits of a, then low 16 bits of b
+__device__ __forceinline__ uint32_t pack_lo16(uint32_t a, uint32_t b) {
+  return __builtin_amdgcn_perm(b, a, 0x05040100u);
+}
 
 // v_med3_u32 (written out: the min/max form gets CSE'd with the column
 // min3/max3 and loses the 3-input instructions)
@@ -487,63 +507,92 @@ __device__ __forceinline__ int clahe_cell_index(int p, float inv) {
   return (int)floorf((float)p * inv - 0.5f);
 }
 
+// CLAHE_Interpolation_Body, x part: weights {xa1, xa} and the cell column
+// offset (x 256) of image column gx.
+__device__ __forceinline__ void clahe_x(int gx, float inv_tw, int cx0, f32x2& xw, int& xoff) {
+  const float fx = (float)gx * inv_tw - 0.5f;
+  const int ix = (int)floorf(fx);
+  const float xa = fx - (float)ix;
+  xw = f32x2{1.0f - xa, xa};
+  xoff = (ix - cx0) * 256;
+}
+
+// y part for image row y (clamped): weights {ya1, ya} and the cell row.
+__device__ __forceinline__ const uint32_t* clahe_row(int y, int H, float inv_th, int cy0, int ncx,
+                                                     const uint32_t* cells, f32x2& yw) {
+  const int gy = min(max(y, 0), H - 1);
+  const float fy = (float)gy * inv_th - 0.5f;
+  const int iy = (int)floorf(fy);
+  const float ya = fy - (float)iy;
+  yw = f32x2{1.0f - ya, ya};
+  return cells + (iy - cy0) * ncx * 256;
+}
+
+// One pixel: bgr_to_ycrcb, the blended LUT luma y2, and the ycrcb_to_bgr
+// terms x4 for ycc_pair.  Cr/Cb are kept as Cr-128 / Cb-128: for arithmetic
+// shifts (v + (128 << 14)) >> 14 == (v >> 14) + 128, so the u8 saturation
+// becomes one clamp to [-128, 127] (Y itself is always <= 255).
+__device__ __forceinline__ void clahe_ycc(int bb, int gg, int rr, const uint32_t* cell, f32x2 xw,
+                                          f32x2 yw, uint32_t& y2, int& tb, int& tg, int& tr) {
+  const int Y = bgr_to_y(bb, gg, rr);
+  const int dcr = min(max(((rr - Y) * 11682 + 8192) >> 14, -128), 127);
+  const int dcb = min(max(((bb - Y) * 9241 + 8192) >> 14, -128), 127);
+  const uint32_t q = cell[Y];
+  // (l11*xa1 + l12*xa, l21*xa1 + l22*xa) as one packed-f32 pair, then
+  // top*ya1 + bottom*ya: the scalar expression's exact op order
+  const f32x2 l1 = {(float)(q & 255), (float)((q >> 16) & 255)};
+  const f32x2 l2 = {(float)((q >> 8) & 255), (float)(q >> 24)};
+  const f32x2 tt = l1 * xw.x + l2 * xw.y;
+  const f32x2 tw = tt * yw;
+  // a convex blend of u8 LUT entries: cvRound lands in [0, 255], so the
+  // saturate_cast is the identity
+  y2 = (uint32_t)__float2int_rn(tw.x + tw.y);
+  tb = dcb * (29049 * 4) + 8192 * 4;
+  tg = dcb * (-5636 * 4) + dcr * (-11698 * 4) + 8192 * 4;
+  tr = dcr * (22987 * 4) + 8192 * 4;
+}
+
 template <bool CLAHE, bool LB>
 __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ in,
                                                    uint8_t* __restrict__ out,
                                                    const uint8_t* __restrict__ lut, int H, int W,
                                                    int pitch, int vec, ClaheGeo g, LbFuse lb) {
-  constexpr int kUnion = CLAHE ? (LB ? (kCellMax * 1024 > kM3H * kM3OStride ? kCellMax * 1024
-                                                                             : kM3H * kM3OStride)
-                                     : kCellMax * 1024)
-                               : (LB ? kM3H * kM3OStride : 16);
-  __shared__ __attribute__((aligned(16))) uint8_t tile[kM3TH * kM3Stride];
-  __shared__ __attribute__((aligned(16))) uint8_t uni[kUnion];  // cells, then the median tile
-  uint32_t* cells = (uint32_t*)uni;
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kM3TH * kM3Stride];  // halo, then medians
+  extern __shared__ __attribute__((aligned(16))) uint32_t cells[];  // CLAHE cells (host-sized)
 
   const int tid = threadIdx.x;
-  const int b = blockIdx.z;
-  const int x0 = blockIdx.x * kM3W, y0 = blockIdx.y * kM3H;
+  // XCD-aware tile order: workgroups go round-robin to the 8 XCDs, so
+  // dispatch slot L runs on XCD L % 8; give each XCD one contiguous run of
+  // tiles (row-major within a frame) so the halo rows and the 12-byte side
+  // halos shared by neighbouring tiles hit that XCD's L2.
+  int b, x0, y0;
+  {
+    const int ntx = (W + kM3W - 1) / kM3W, nty = (H + kM3H - 1) / kM3H;
+    const int n = gridDim.x, L = blockIdx.x;
+    const int q = n >> 3, r = n & 7, xcd = L & 7, slot = L >> 3;
+    const int t = xcd < r ? xcd * (q + 1) + slot : r * (q + 1) + (xcd - r) * q + slot;
+    b = t / (ntx * nty);
+    const int f = t - b * (ntx * nty);
+    y0 = (f / ntx) * kM3H;
+    x0 = (f - (f / ntx) * ntx) * kM3W;
+  }
   const uint8_t* frame = in + (size_t)b * H * pitch;
 
-  // ---- 1. packed LUT cells of this block
-  int cx0 = 0, cy0 = 0, ncx = 1;
-  if constexpr (CLAHE) {
-    const int gx_lo = max(x0 - 4, 0), gx_hi = min(x0 + kM3TW - 5, W - 1);
-    const int gy_lo = max(y0 - 1, 0), gy_hi = min(y0 + kM3H, H - 1);
-    cx0 = clahe_cell_index(gx_lo, g.inv_tw);
-    cy0 = clahe_cell_index(gy_lo, g.inv_th);
-    ncx = clahe_cell_index(gx_hi, g.inv_tw) - cx0 + 1;
-    const int ncy = clahe_cell_index(gy_hi, g.inv_th) - cy0 + 1;
-    const uint8_t* flut = lut + (size_t)b * g.tiles * g.tiles * 256;
-    const int Y = tid;  // one LUT entry per thread per cell
-    for (int c = 0; c < ncx * ncy; ++c) {
-      const int cy = c / ncx, cx = c - (c / ncx) * ncx;
-      const int iy = cy0 + cy, ix = cx0 + cx;
-      const int r1 = max(iy, 0), r2 = min(iy + 1, g.tiles - 1);
-      const int c1 = max(ix, 0), c2 = min(ix + 1, g.tiles - 1);
-      const uint32_t l11 = flut[(r1 * g.tiles + c1) * 256 + Y];
-      const uint32_t l12 = flut[(r1 * g.tiles + c2) * 256 + Y];
-      const uint32_t l21 = flut[(r2 * g.tiles + c1) * 256 + Y];
-      const uint32_t l22 = flut[(r2 * g.tiles + c2) * 256 + Y];
-      cells[c * 256 + Y] = l11 | (l12 << 8) | (l21 << 16) | (l22 << 24);
-    }
-  }
-
-  // ---- 2. halo tile: thread -> one 4-pixel column group (gc) and the rows
-  //      r0, r0+7, ... (so the per-pixel x interpolation is computed once);
-  //      every load is issued before any use.
-  constexpr int kRowStep = 256 / kM3Groups;  // 7 (238 threads busy)
-  constexpr int kIt = (kM3TH + kRowStep - 1) / kRowStep;  // 5
-  const int gc = tid % kM3Groups, r0 = tid / kM3Groups;
-  const bool s2 = r0 < kRowStep;
-  const int px0 = x0 - 4 + gc * 4;
-  const bool vrow = vec && px0 >= 0 && px0 + 3 < W;
+  // ---- 1. halo loads.  Thread -> 4-pixel group gc = tid & 31 (px x0+4gc ..
+  //      x0+4gc+3) of rows rs, rs+8, rs+16, rs+24 and, in wave 0 only, 32+rs;
+  //      the side columns x0-1 and x0+128 are 68 single pixels for threads
+  //      64..131.  Every load is issued before any use.  In the tile, group
+  //      gc sits at byte 12*(gc+1) and the side pixels at bytes 9 and 396.
+  constexpr int kIt = 5;
+  const int gc = tid & 31, rs = tid >> 5;
+  const int px0 = x0 + gc * 4;
+  const bool vrow = vec && px0 + 3 < W;
   uint32_t d[kIt][3];
 #pragma unroll
   for (int it = 0; it < kIt; ++it) {
-    const int hr = r0 + it * kRowStep;
+    const int hr = rs + 8 * it;  // < 32 for it < 4; it == 4: wave 0 only
     d[it][0] = d[it][1] = d[it][2] = 0;
-    if (s2 && hr < kM3TH) {
+    if (hr < kM3TH) {
       const int gy = min(max(y0 - 1 + hr, 0), H - 1);
       const uint8_t* row = frame + (size_t)gy * pitch;
       if (vrow) {
@@ -555,7 +604,7 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
         uint8_t v[12];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int gx = min(max(px0 + j, 0), W - 1);
+          const int gx = min(px0 + j, W - 1);
           v[3 * j] = row[gx * 3];
           v[3 * j + 1] = row[gx * 3 + 1];
           v[3 * j + 2] = row[gx * 3 + 2];
@@ -567,67 +616,110 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
       }
     }
   }
+  const int sk = tid - 64;  // side pixel: row sk >> 1, right column if sk & 1
+  const bool side = sk >= 0 && sk < 2 * kM3TH;
+  const int s_hr = sk >> 1, s_px = (sk & 1) ? min(x0 + kM3W, W - 1) : max(x0 - 1, 0);
+  int sb = 0, sg = 0, sr = 0;
+  if (side) {
+    const uint8_t* sp = frame + (size_t)min(max(y0 - 1 + s_hr, 0), H - 1) * pitch + s_px * 3;
+    sb = sp[0];
+    sg = sp[1];
+    sr = sp[2];
+  }
+
+  // ---- 2. packed LUT cells of this block: wave w builds cells w, w+4, ..;
+  //      lane l gathers Y = 4l..4l+3 of the 4 tile LUTs with one dword load
+  //      each and transposes the 4x4 bytes with v_perm_b32.
+  int cx0 = 0, cy0 = 0, ncx = 1;
+  if constexpr (CLAHE) {
+    const int gx_lo = max(x0 - 1, 0), gx_hi = min(x0 + kM3W, W - 1);
+    const int gy_lo = max(y0 - 1, 0), gy_hi = min(y0 + kM3H, H - 1);
+    cx0 = clahe_cell_index(gx_lo, g.inv_tw);
+    cy0 = clahe_cell_index(gy_lo, g.inv_th);
+    ncx = clahe_cell_index(gx_hi, g.inv_tw) - cx0 + 1;
+    const int ncy = clahe_cell_index(gy_hi, g.inv_th) - cy0 + 1;
+    const uint32_t* flut = (const uint32_t*)(lut + (size_t)b * g.tiles * g.tiles * 256);
+    const int lane = tid & 63;
+    for (int c = tid >> 6; c < ncx * ncy; c += 4) {
+      const int cy = c / ncx, cx = c - (c / ncx) * ncx;
+      const int iy = cy0 + cy, ix = cx0 + cx;
+      const int r1 = max(iy, 0), r2 = min(iy + 1, g.tiles - 1);
+      const int c1 = max(ix, 0), c2 = min(ix + 1, g.tiles - 1);
+      const uint32_t l11 = flut[(r1 * g.tiles + c1) * 64 + lane];
+      const uint32_t l12 = flut[(r1 * g.tiles + c2) * 64 + lane];
+      const uint32_t l21 = flut[(r2 * g.tiles + c1) * 64 + lane];
+      const uint32_t l22 = flut[(r2 * g.tiles + c2) * 64 + lane];
+      const uint32_t p_lo = __builtin_amdgcn_perm(l12, l11, 0x05010400u);  // a0 b0 a1 b1
+      const uint32_t p_hi = __builtin_amdgcn_perm(l12, l11, 0x07030602u);  // a2 b2 a3 b3
+      const uint32_t q_lo = __builtin_amdgcn_perm(l22, l21, 0x05010400u);
+      const uint32_t q_hi = __builtin_amdgcn_perm(l22, l21, 0x07030602u);
+      uint4 v;
+      v.x = __builtin_amdgcn_perm(q_lo, p_lo, 0x05040100u);
+      v.y = __builtin_amdgcn_perm(q_lo, p_lo, 0x07060302u);
+      v.z = __builtin_amdgcn_perm(q_hi, p_hi, 0x05040100u);
+      v.w = __builtin_amdgcn_perm(q_hi, p_hi, 0x07060302u);
+      *(uint4*)(cells + c * 256 + 4 * lane) = v;
+    }
+  }
+
+  // ---- 3. CLAHE in registers -> LDS
   // per-pixel x interpolation (CLAHE_Interpolation_Body xa/xa1/ind)
   f32x2 xw[4];   // {xa1, xa}
   int xoff[4];   // cell column offset * 256
   if constexpr (CLAHE) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int gx = min(max(px0 + j, 0), W - 1);
-      const float fx = (float)gx * g.inv_tw - 0.5f;
-      const int ix = (int)floorf(fx);
-      const float xa = fx - (float)ix;
-      xw[j] = f32x2{1.0f - xa, xa};
-      xoff[j] = (ix - cx0) * 256;
-    }
+    for (int j = 0; j < 4; ++j) clahe_x(min(px0 + j, W - 1), g.inv_tw, cx0, xw[j], xoff[j]);
     __syncthreads();  // cells visible
   }
 #pragma unroll
   for (int it = 0; it < kIt; ++it) {
-    const int hr = r0 + it * kRowStep;
-    if (!s2 || hr >= kM3TH) break;
-    uint32_t* dst = (uint32_t*)(tile + hr * kM3Stride + gc * 12);
+    const int hr = rs + 8 * it;
+    if (hr >= kM3TH) break;
+    uint32_t* dst = (uint32_t*)(tile + hr * kM3Stride + (gc + 1) * 12);
     if constexpr (CLAHE) {
-      const int gy = min(max(y0 - 1 + hr, 0), H - 1);
-      const float fy = (float)gy * g.inv_th - 0.5f;
-      const int iy = (int)floorf(fy);
-      const float ya = fy - (float)iy;
-      const f32x2 yw = {1.0f - ya, ya};
-      const uint32_t* crow = cells + (iy - cy0) * ncx * 256;
-      uint32_t o[3] = {0, 0, 0};
+      f32x2 yw;
+      const uint32_t* crow = clahe_row(y0 - 1 + hr, H, g.inv_th, cy0, ncx, cells, yw);
+      uint32_t y2[4];
+      int tb[4], tg[4], tr[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int bb = (d[it][(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255;
         const int gg = (d[it][(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255;
         const int rr = (d[it][(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255;
-        int Y, Cr, Cb;
-        bgr_to_ycrcb(bb, gg, rr, Y, Cr, Cb);
-        const uint32_t q = crow[xoff[j] + Y];
-        // (l11*xa1 + l12*xa, l21*xa1 + l22*xa) as one packed-f32 pair, then
-        // top*ya1 + bottom*ya: the scalar expression's exact op order
-        const f32x2 l1 = {(float)(q & 255), (float)((q >> 16) & 255)};
-        const f32x2 l2 = {(float)((q >> 8) & 255), (float)(q >> 24)};
-        const f32x2 tb = l1 * xw[j].x + l2 * xw[j].y;
-        const f32x2 tw = tb * yw;
-        const int y2 = sat_u8(__float2int_rn(tw.x + tw.y));
-        int ob, og, orr;
-        ycrcb_to_bgr(y2, Cr, Cb, ob, og, orr);
-        o[(3 * j) >> 2] |= (uint32_t)ob << (8 * ((3 * j) & 3));
-        o[(3 * j + 1) >> 2] |= (uint32_t)og << (8 * ((3 * j + 1) & 3));
-        o[(3 * j + 2) >> 2] |= (uint32_t)orr << (8 * ((3 * j + 2) & 3));
+        clahe_ycc(bb, gg, rr, crow + xoff[j], xw[j], yw, y2[j], tb[j], tg[j], tr[j]);
       }
-      dst[0] = o[0];
-      dst[1] = o[1];
-      dst[2] = o[2];
+      // bytes b0 g0 r0 b1 | g1 r1 b2 g2 | r2 b3 g3 r3 as six channel pairs
+      dst[0] = pack_lo16(ycc_pair(tb[0], tg[0], y2[0], y2[0]), ycc_pair(tr[0], tb[1], y2[0], y2[1]));
+      dst[1] = pack_lo16(ycc_pair(tg[1], tr[1], y2[1], y2[1]), ycc_pair(tb[2], tg[2], y2[2], y2[2]));
+      dst[2] = pack_lo16(ycc_pair(tr[2], tb[3], y2[2], y2[3]), ycc_pair(tg[3], tr[3], y2[3], y2[3]));
     } else {
       dst[0] = d[it][0];
       dst[1] = d[it][1];
       dst[2] = d[it][2];
     }
   }
+  if (side) {
+    uint8_t* dst = tile + s_hr * kM3Stride + ((sk & 1) ? 12 * (kM3W / 4 + 1) : 9);
+    if constexpr (CLAHE) {
+      f32x2 sxw, yw;
+      int sxoff;
+      clahe_x(s_px, g.inv_tw, cx0, sxw, sxoff);
+      const uint32_t* crow = clahe_row(y0 - 1 + s_hr, H, g.inv_th, cy0, ncx, cells, yw);
+      uint32_t y2;
+      int tb, tg, tr;
+      clahe_ycc(sb, sg, sr, crow + sxoff, sxw, yw, y2, tb, tg, tr);
+      const uint32_t bg = ycc_pair(tb, tg, y2, y2), rr = ycc_pair(tr, tr, y2, y2);
+      sb = bg & 255;
+      sg = (bg >> 8) & 255;
+      sr = rr & 255;
+    }
+    dst[0] = (uint8_t)sb;
+    dst[1] = (uint8_t)sg;
+    dst[2] = (uint8_t)sr;
+  }
   __syncthreads();
 
-  // ---- 3. medians: thread -> 4 px (rx..rx+3) x 4 rows (ry..ry+3)
+  // ---- 4. medians: thread -> 4 px (rx..rx+3) x 4 rows (ry..ry+3)
   const int rx = (tid & 31) * 4, ry = (tid >> 5) * 4;
   uint32_t rw[6][5];
 #pragma unroll
@@ -636,6 +728,7 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
 #pragma unroll
     for (int j = 0; j < 5; ++j) rw[r][j] = p[j];
   }
+  if constexpr (LB) __syncthreads();  // the halo tile is in registers: reuse it for medians
   // byte (column jj in 0..5 = px rx-1+jj, channel c) of row r sits at window
   // byte 1 + 3*jj + c
 #define RV_B(r, k) ((rw[r][(k) >> 2] >> (8 * ((k) & 3))) & 255u)
@@ -667,7 +760,7 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
       }
     }
     if constexpr (LB) {
-      uint32_t* od = (uint32_t*)(uni + (ry + o) * kM3OStride + rx * 3);
+      uint32_t* od = (uint32_t*)(tile + (ry + o) * kM3Stride + rx * 3);
       od[0] = res[0];
       od[1] = res[1];
       od[2] = res[2];
@@ -686,8 +779,8 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
   }
 #undef RV_B
 
-  // ---- 4. letterbox pixels owned by this block: per-axis taps once into
-  //      LDS (after the cells region, which is free again), then 2-D
+  // ---- 5. letterbox pixels owned by this block: per-axis taps once into
+  //      LDS, then 2-D from the median tile
   if constexpr (LB) {
     __shared__ LbTap tapx[kM3W + 8], tapy[kM3H + 8];
     __shared__ int ntap[2], dlo[2];
@@ -706,35 +799,49 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
     if (tid < nx) tapx[tid] = lb_tap_x(dlo[0] + tid, G.scale_x, W);
     else if (tid >= 192 && tid - 192 < ny) tapy[tid - 192] = lb_tap_y(dlo[1] + tid - 192, G.scale_y, H);
     __syncthreads();
-    uint8_t* lbo = lb.out + (size_t)b * G.out_h * G.out_w * 3;
-    for (int i = tid; i < nx * ny; i += 256) {
-      const int jy = i / nx, jx = i - (i / nx) * nx;
-      const LbTap tx = tapx[jx], ty = tapy[jy];
+    // lane -> letterbox column jx, wave -> rows jy = w, w+4, ..: the row's
+    // ownership test is wave-uniform, the tap tables are read once per lane
+    const size_t orow = (size_t)G.out_w * 3;
+    uint8_t* lbo = lb.out + ((size_t)b * G.out_h + G.top + dlo[1]) * orow +
+                   (size_t)(G.left + dlo[0]) * 3;
+    for (int jx = tid & 63; jx < nx; jx += 64) {
+      const LbTap tx = tapx[jx];
       // owner: the block holding the first tap (host checked: all taps)
-      if (tx.s0 < x0 || tx.s0 >= x0 + kM3W || ty.s0 < y0 || ty.s0 >= y0 + kM3H) continue;
-      const uint8_t* r0 = uni + (ty.s0 - y0) * kM3OStride;
-      const uint8_t* r1 = uni + (ty.s1 - y0) * kM3OStride;
+      const bool own_x = tx.s0 >= x0 && tx.s0 < x0 + kM3W;
       const int c0 = (tx.s0 - x0) * 3, c1 = (tx.s1 - x0) * 3;
-      uint8_t* dst = lbo + ((size_t)(G.top + dlo[1] + jy) * G.out_w + G.left + dlo[0] + jx) * 3;
+      for (int jy = tid >> 6; jy < ny; jy += 4) {
+        const LbTap ty = tapy[jy];
+        if (ty.s0 < y0 || ty.s0 >= y0 + kM3H || !own_x) continue;
+        const uint8_t* r0 = tile + (ty.s0 - y0) * kM3Stride;
+        const uint8_t* r1 = tile + (ty.s1 - y0) * kM3Stride;
+        uint8_t* dst = lbo + jy * orow + jx * 3;
+        // lb_vmix with 24-bit multiplies (u8 x 11-bit weights, (d >> 4) <
+        // 2^15): the full-rate v_mul_u32_u24 instead of v_mul_lo_u32
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const int d0 = r0[c0 + c] * tx.w0 + r0[c1 + c] * tx.w1;
-        const int d1 = r1[c0 + c] * tx.w0 + r1[c1 + c] * tx.w1;
-        dst[c] = (uint8_t)lb_vmix(d0, d1, ty.w0, ty.w1);
+        for (int c = 0; c < 3; ++c) {
+          const uint32_t d0 = __umul24(r0[c0 + c], tx.w0) + __umul24(r0[c1 + c], tx.w1);
+          const uint32_t d1 = __umul24(r1[c0 + c], tx.w0) + __umul24(r1[c1 + c], tx.w1);
+          dst[c] = (uint8_t)(((__umul24(ty.w0, d0 >> 4) >> 16) + (__umul24(ty.w1, d1 >> 4) >> 16) + 2) >> 2);
+        }
       }
     }
   }
 }
 
 // Host checks for med3_kernel.
-static bool med3_cells_fit(const ClaheGeo& g, int H, int W) {
-  // distinct floor(p/t - 0.5) over a span of n consecutive p <= ceil(n/t) + 1
-  // (+1 more for float rounding of p * inv)
+// Upper bound of ncx * ncy in the kernel: distinct floor(p/t - 0.5) over a
+// span of n consecutive p <= ceil(n/t) + 1 (+1 more for float rounding of
+// p * inv), and at most tiles + 1 values (-1 .. tiles-1).
+static int med3_cells(const ClaheGeo& g) {
   const int ncx = min((kM3TW + g.tw - 1) / g.tw + 2, g.tiles + 1);
   const int ncy = min((kM3TH + g.th - 1) / g.th + 2, g.tiles + 1);
+  return ncx * ncy;
+}
+
+static bool med3_cells_fit(const ClaheGeo& g, int H, int W) {
   (void)H;
   (void)W;
-  return ncx * ncy <= kCellMax;
+  return med3_cells(g) <= kCellMax;
 }
 
 // every letterbox pixel's nonzero taps must lie in the block of its first tap
@@ -757,8 +864,9 @@ template <bool CLAHE, bool LB>
 static void launch_med3(const uint8_t* in, uint8_t* out, const uint8_t* lut, int B, int H, int W,
                         int pitch, const ClaheGeo& g, const LbFuse& lb, hipStream_t s) {
   const int vec = (pitch % 4 == 0) && (((uintptr_t)in) % 4 == 0) && (((uintptr_t)out) % 4 == 0);
-  dim3 grid(ceil_div(W, kM3W), ceil_div(H, kM3H), B);
-  med3_kernel<CLAHE, LB><<<grid, 256, 0, s>>>(in, out, lut, H, W, pitch, vec, g, lb);
+  const dim3 grid(ceil_div(W, kM3W) * ceil_div(H, kM3H) * B);  // tiles, mapped in the kernel
+  const size_t cell_bytes = CLAHE ? (size_t)med3_cells(g) * 1024 : 0;
+  med3_kernel<CLAHE, LB><<<grid, 256, cell_bytes, s>>>(in, out, lut, H, W, pitch, vec, g, lb);
 }
 
 // Gray span for the low-contrast gate (pipeline.py:24-30).
