@@ -69,16 +69,19 @@ __device__ __forceinline__ int clahe_luma(int b, int g, int r) {
 // One 256-thread workgroup per tile.  16 LDS histogram copies (wave x lane
 // & 3), bin-major so the copies of one bin sit in 16 different banks: equal
 // Y values in a wave (flat sky / asphalt) spread over 4 addresses instead of
-// serialising on one, with no bank conflicts between the copies.
+// serialising on one, with no bank conflicts between the copies.  (One
+// copy per lane with packed u16 counters -- conflict-free for any Y -- was
+// measured slower: 47.5 vs 42.2 us at 32 x 1080p, the 33 KB of LDS halves
+// the resident blocks of this load-bound pass.)
 // ---------------------------------------------------------------------------
 template <int SPACE>
 __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restrict__ in,
                                                         uint8_t* __restrict__ lut, int H, int W,
                                                         int pitch, ClaheGeo g) {
   constexpr int kCopies = 16;
-  __shared__ int hist[256 * kCopies];
-  __shared__ int scan[256];
-  __shared__ int wsum[4];
+  constexpr int kWords = 256 * kCopies;
+  __shared__ int hist[kWords];
+  __shared__ int wsum[4], wtot[4];
   const int t = threadIdx.x;
   const int wave = t >> 6;
   const int tile = blockIdx.x;
@@ -87,13 +90,14 @@ __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restric
   const int x0 = tx * g.tw, y0 = ty * g.th;
   const uint8_t* frame = in + (size_t)b * H * pitch;
 
-  for (int i = t; i < kCopies * 256; i += 256) hist[i] = 0;
+  for (int i = t; i < kWords; i += 256) hist[i] = 0;
   __syncthreads();
 
   const bool inside = (x0 + g.tw <= W) && (y0 + g.th <= H);
   const bool vec = inside && (g.tw % 4 == 0) && (pitch % 4 == 0) &&
                    ((((uintptr_t)frame) + (uintptr_t)x0 * 3) % 4 == 0);
   int* h = hist + ((wave << 2) | (t & 3));  // bin y -> h[y * kCopies]
+  auto bump = [&](int y) { atomicAdd(&h[y * kCopies], 1); };
   if (vec) {
     const int groups = g.tw >> 2;
     const int total = groups * g.th;
@@ -119,10 +123,10 @@ __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restric
         if (i0 + u * 256 >= total) break;
         const uint32_t w0 = w[u][0], w1 = w[u][1], w2 = w[u][2];
         // bytes little-endian: w0 = b0 g0 r0 b1 | w1 = g1 r1 b2 g2 | w2 = r2 b3 g3 r3
-        atomicAdd(&h[clahe_luma<SPACE>(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255) * kCopies], 1);
-        atomicAdd(&h[clahe_luma<SPACE>(w0 >> 24, w1 & 255, (w1 >> 8) & 255) * kCopies], 1);
-        atomicAdd(&h[clahe_luma<SPACE>((w1 >> 16) & 255, w1 >> 24, w2 & 255) * kCopies], 1);
-        atomicAdd(&h[clahe_luma<SPACE>((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24) * kCopies], 1);
+        bump(clahe_luma<SPACE>(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255));
+        bump(clahe_luma<SPACE>(w0 >> 24, w1 & 255, (w1 >> 8) & 255));
+        bump(clahe_luma<SPACE>((w1 >> 16) & 255, w1 >> 24, w2 & 255));
+        bump(clahe_luma<SPACE>((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24));
       }
     }
   } else {
@@ -135,7 +139,7 @@ __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restric
       int sx = x0 + c;
       if (sx >= W) sx = reflect101(sx, W);
       const uint8_t* p = frame + (size_t)sy * pitch + (size_t)sx * 3;
-      atomicAdd(&h[clahe_luma<SPACE>(p[0], p[1], p[2]) * kCopies], 1);
+      bump(clahe_luma<SPACE>(p[0], p[1], p[2]));
     }
   }
   __syncthreads();
@@ -160,17 +164,23 @@ __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restric
       if (t % step == 0 && t / step < residual) v += 1;
     }
   }
-  // inclusive prefix sum over the 256 bins (Hillis-Steele in LDS)
-  scan[t] = v;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    int add = t >= off ? scan[t - off] : 0;
-    __syncthreads();
-    scan[t] += add;
-    __syncthreads();
+  // inclusive prefix sum over the 256 bins: wave scans, then the totals of
+  // the lower waves
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(v, off);
+    if ((t & 63) >= off) v += y;
   }
-  const float f = (float)scan[t] * g.lut_scale;
+  if ((t & 63) == 63) wtot[wave] = v;
+  __syncthreads();
+  for (int w = 0; w < wave; ++w) v += wtot[w];
+  const float f = (float)v * g.lut_scale;
   lut[((size_t)b * g.tiles * g.tiles + tile) * 256 + t] = (uint8_t)sat_u8(__float2int_rn(f));
+}
+
+template <int SPACE>
+static void launch_clahe_lut(const uint8_t* in, uint8_t* lut, int B, int H, int W, int pitch,
+                             const ClaheGeo& g, hipStream_t s) {
+  clahe_lut_kernel<SPACE><<<dim3(g.tiles * g.tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
 }
 
 // CLAHE_Interpolation_Body per-axis coefficients.
@@ -475,14 +485,24 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 // Two output channels of ycrcb_to_bgr at once.  lo4/hi4 are the channel
 // terms scaled by 4 ((4x) >> 16 == x >> 14, so each term is the high half);
 // one v_perm_b32 gathers both, v_pk_add_u16 adds the luma of each half
+// (ylo / yhi: only their low 16 bits count)
 // (|y + term| < 2^15, so the i16 view is exact) and v_sat_pk_u8_i16
 // saturates and packs: bytes {sat(ylo + lo), sat(yhi + hi)} in the low half.
 __device__ __forceinline__ uint32_t ycc_pair(int lo4, int hi4, uint32_t ylo, uint32_t yhi) {
   const uint32_t t = __builtin_amdgcn_perm((uint32_t)hi4, (uint32_t)lo4, 0x07060302u);
-  const u16x2 s = __builtin_bit_cast(u16x2, t) + __builtin_bit_cast(u16x2, ylo | (yhi << 16));
+  const uint32_t y = __builtin_amdgcn_perm(yhi, ylo, 0x05040100u);  // low halves
+  const u16x2 s = __builtin_bit_cast(u16x2, t) + __builtin_bit_cast(u16x2, y);
   uint32_t r;
   asm("v_sat_pk_u8_i16 %0, %1" : "=v"(r) : "v"(__builtin_bit_cast(uint32_t, s)));
   return r;
+}
+
+// four values < 256 -> one dword (a in byte 0): three v_perm_b32
+// (selector byte 0x0c yields zero)
+__device__ __forceinline__ uint32_t pack_u8x4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const uint32_t ab = __builtin_amdgcn_perm(b, a, 0x0c0c0400u);
+  const uint32_t cd = __builtin_amdgcn_perm(d, c, 0x0c0c0400u);
+  return __builtin_amdgcn_perm(cd, ab, 0x05040100u);
 }
 
 // low 16 bits of a, then low 16 bits of b
@@ -507,14 +527,14 @@ __device__ __forceinline__ int clahe_cell_index(int p, float inv) {
   return (int)floorf((float)p * inv - 0.5f);
 }
 
-// CLAHE_Interpolation_Body, x part: weights {xa1, xa} and the cell column
-// offset (x 256) of image column gx.
-__device__ __forceinline__ void clahe_x(int gx, float inv_tw, int cx0, f32x2& xw, int& xoff) {
+// CLAHE_Interpolation_Body, x part: weights {xa1, xa} and the byte offset
+// of image column gx's cell column (cells are 256 x u32).
+__device__ __forceinline__ void clahe_x(int gx, float inv_tw, int cx0, f32x2& xw, int& xoffb) {
   const float fx = (float)gx * inv_tw - 0.5f;
   const int ix = (int)floorf(fx);
   const float xa = fx - (float)ix;
   xw = f32x2{1.0f - xa, xa};
-  xoff = (ix - cx0) * 256;
+  xoffb = (ix - cx0) * 1024;
 }
 
 // y part for image row y (clamped): weights {ya1, ya} and the cell row.
@@ -528,16 +548,17 @@ __device__ __forceinline__ const uint32_t* clahe_row(int y, int H, float inv_th,
   return cells + (iy - cy0) * ncx * 256;
 }
 
-// One pixel: bgr_to_ycrcb, the blended LUT luma y2, and the ycrcb_to_bgr
-// terms x4 for ycc_pair.  Cr/Cb are kept as Cr-128 / Cb-128: for arithmetic
+// One pixel: bgr_to_ycrcb, the blended LUT luma y2 (in the low 16 bits of
+// y2, see below), and the ycrcb_to_bgr terms x4 for ycc_pair.  `cellx` is
+// the cell row plus the pixel's cell column, in bytes.  Cr/Cb are kept as Cr-128 / Cb-128: for arithmetic
 // shifts (v + (128 << 14)) >> 14 == (v >> 14) + 128, so the u8 saturation
 // becomes one clamp to [-128, 127] (Y itself is always <= 255).
-__device__ __forceinline__ void clahe_ycc(int bb, int gg, int rr, const uint32_t* cell, f32x2 xw,
+__device__ __forceinline__ void clahe_ycc(int bb, int gg, int rr, const uint8_t* cellx, f32x2 xw,
                                           f32x2 yw, uint32_t& y2, int& tb, int& tg, int& tr) {
   const int Y = bgr_to_y(bb, gg, rr);
   const int dcr = min(max(((rr - Y) * 11682 + 8192) >> 14, -128), 127);
   const int dcb = min(max(((bb - Y) * 9241 + 8192) >> 14, -128), 127);
-  const uint32_t q = cell[Y];
+  const uint32_t q = *(const uint32_t*)(cellx + Y * 4);
   // (l11*xa1 + l12*xa, l21*xa1 + l22*xa) as one packed-f32 pair, then
   // top*ya1 + bottom*ya: the scalar expression's exact op order
   const f32x2 l1 = {(float)(q & 255), (float)((q >> 16) & 255)};
@@ -545,8 +566,10 @@ __device__ __forceinline__ void clahe_ycc(int bb, int gg, int rr, const uint32_t
   const f32x2 tt = l1 * xw.x + l2 * xw.y;
   const f32x2 tw = tt * yw;
   // a convex blend of u8 LUT entries: cvRound lands in [0, 255], so the
-  // saturate_cast is the identity
-  y2 = (uint32_t)__float2int_rn(tw.x + tw.y);
+  // saturate_cast is the identity.  cvRound (half-even) by the 1.5 * 2^23
+  // addend: the f32 add rounds to an integer, which then sits in the low
+  // mantissa bits; only the low 16 bits of y2 are used (ycc_pair).
+  y2 = __float_as_uint((tw.x + tw.y) + 12582912.0f);
   tb = dcb * (29049 * 4) + 8192 * 4;
   tg = dcb * (-5636 * 4) + dcr * (-11698 * 4) + 8192 * 4;
   tr = dcr * (22987 * 4) + 8192 * 4;
@@ -665,7 +688,7 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
   // ---- 3. CLAHE in registers -> LDS
   // per-pixel x interpolation (CLAHE_Interpolation_Body xa/xa1/ind)
   f32x2 xw[4];   // {xa1, xa}
-  int xoff[4];   // cell column offset * 256
+  int xoff[4];   // cell column byte offset
   if constexpr (CLAHE) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) clahe_x(min(px0 + j, W - 1), g.inv_tw, cx0, xw[j], xoff[j]);
@@ -686,7 +709,7 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
         const int bb = (d[it][(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255;
         const int gg = (d[it][(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255;
         const int rr = (d[it][(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255;
-        clahe_ycc(bb, gg, rr, crow + xoff[j], xw[j], yw, y2[j], tb[j], tg[j], tr[j]);
+        clahe_ycc(bb, gg, rr, (const uint8_t*)crow + xoff[j], xw[j], yw, y2[j], tb[j], tg[j], tr[j]);
       }
       // bytes b0 g0 r0 b1 | g1 r1 b2 g2 | r2 b3 g3 r3 as six channel pairs
       dst[0] = pack_lo16(ycc_pair(tb[0], tg[0], y2[0], y2[0]), ycc_pair(tr[0], tb[1], y2[0], y2[1]));
@@ -707,7 +730,7 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
       const uint32_t* crow = clahe_row(y0 - 1 + s_hr, H, g.inv_th, cy0, ncx, cells, yw);
       uint32_t y2;
       int tb, tg, tr;
-      clahe_ycc(sb, sg, sr, crow + sxoff, sxw, yw, y2, tb, tg, tr);
+      clahe_ycc(sb, sg, sr, (const uint8_t*)crow + sxoff, sxw, yw, y2, tb, tg, tr);
       const uint32_t bg = ycc_pair(tb, tg, y2, y2), rr = ycc_pair(tr, tr, y2, y2);
       sb = bg & 255;
       sg = (bg >> 8) & 255;
@@ -732,12 +755,13 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
   // byte (column jj in 0..5 = px rx-1+jj, channel c) of row r sits at window
   // byte 1 + 3*jj + c
 #define RV_B(r, k) ((rw[r][(k) >> 2] >> (8 * ((k) & 3))) & 255u)
-  uint8_t* fout = out + (size_t)b * H * pitch;
   const int x = x0 + rx;
+  // row pointer stepped by pitch (no per-row 64-bit multiply)
+  uint8_t* orow = out + ((size_t)b * H + y0 + ry) * pitch + (size_t)x * 3;
 #pragma unroll
-  for (int o = 0; o < 4; ++o) {
+  for (int o = 0; o < 4; ++o, orow += pitch) {
     const int y = y0 + ry + o;
-    uint32_t res[3] = {0, 0, 0};
+    uint32_t v12[12];  // medians, byte order b0 g0 r0 b1 ...
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       uint32_t lo[6], mi[6], hi[6];
@@ -754,11 +778,12 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
         const uint32_t l = max(max(lo[p], lo[p + 1]), lo[p + 2]);
         const uint32_t m = med3_u32(mi[p], mi[p + 1], mi[p + 2]);
         const uint32_t h = min(min(hi[p], hi[p + 1]), hi[p + 2]);
-        const uint32_t v = med3_u32(l, m, h);
-        const int k = 3 * p + c;
-        res[k >> 2] |= v << (8 * (k & 3));
+        v12[3 * p + c] = med3_u32(l, m, h);
       }
     }
+    uint32_t res[3];
+#pragma unroll
+    for (int w = 0; w < 3; ++w) res[w] = pack_u8x4(v12[4 * w], v12[4 * w + 1], v12[4 * w + 2], v12[4 * w + 3]);
     if constexpr (LB) {
       uint32_t* od = (uint32_t*)(tile + (ry + o) * kM3Stride + rx * 3);
       od[0] = res[0];
@@ -766,7 +791,7 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
       od[2] = res[2];
     }
     if (y < H && x < W) {
-      uint8_t* dst = fout + (size_t)y * pitch + (size_t)x * 3;
+      uint8_t* dst = orow;
       if (vec && x + 3 < W) {
         ((uint32_t*)dst)[0] = res[0];
         ((uint32_t*)dst)[1] = res[1];
@@ -957,7 +982,7 @@ extern "C" int rv_clahe_ycrcb_u8(const uint8_t* in, uint8_t* out, int B, int H, 
   ClaheGeo g = make_geo(H, W, tiles, clip);
   hipStream_t s = as_stream(stream);
   uint8_t* lut = (uint8_t*)ws;
-  clahe_lut_kernel<kYCrCb><<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  launch_clahe_lut<kYCrCb>(in, lut, B, H, W, pitch, g, s);
   clahe_apply_kernel<kYCrCb><<<dim3(1, ceil_div(H, kApplyRows), B), 256, 0, s>>>(in, out, lut, H, W,
                                                                           pitch, g);
   return launch_status("rv_clahe_ycrcb_u8");
@@ -1021,7 +1046,7 @@ extern "C" int rv_clahe_lab_u8(const uint8_t* in, uint8_t* out, int B, int H, in
   ClaheGeo g = make_geo(H, W, tiles, clip);
   hipStream_t s = as_stream(stream);
   uint8_t* lut = (uint8_t*)ws;
-  clahe_lut_kernel<kLab><<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  launch_clahe_lut<kLab>(in, lut, B, H, W, pitch, g, s);
   clahe_apply_kernel<kLab><<<dim3(1, ceil_div(H, kApplyRows), B), 256, 0, s>>>(in, out, lut, H,
                                                                               W, pitch, g);
   return launch_status("rv_clahe_lab_u8");
@@ -1040,7 +1065,7 @@ extern "C" int rv_clahe_median_u8(const uint8_t* in, uint8_t* out, int B, int H,
   hipStream_t s = as_stream(stream);
   uint8_t* lut = (uint8_t*)ws;
   if (k == 3 && med3_cells_fit(g, H, W)) {
-    clahe_lut_kernel<kYCrCb><<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+    launch_clahe_lut<kYCrCb>(in, lut, B, H, W, pitch, g, s);
     launch_med3<true, false>(in, out, lut, B, H, W, pitch, g, LbFuse{}, s);
     return launch_status("rv_clahe_median_u8");
   }
@@ -1048,7 +1073,7 @@ extern "C" int rv_clahe_median_u8(const uint8_t* in, uint8_t* out, int B, int H,
                "LUT window too large for the fused pass (tiles=%d, tile %dx%d); "
                "use rv_clahe_ycrcb_u8 + rv_median_u8c3",
                tiles, g.tw, g.th);
-  clahe_lut_kernel<kYCrCb><<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  launch_clahe_lut<kYCrCb>(in, lut, B, H, W, pitch, g, s);
   dispatch_median<true>(k, in, out, lut, B, H, W, pitch, g, s);
   return launch_status("rv_clahe_median_u8");
 }
@@ -1088,7 +1113,7 @@ extern "C" int rv_clahe_median_letterbox_u8(const uint8_t* in, uint8_t* out, int
   uint8_t* lut = (uint8_t*)ws;
   st = launch_letterbox_pad(lb_out, B, lb.g, s);
   if (st) return st;
-  clahe_lut_kernel<kYCrCb><<<dim3(tiles * tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  launch_clahe_lut<kYCrCb>(in, lut, B, H, W, pitch, g, s);
   launch_med3<true, true>(in, out, lut, B, H, W, pitch, g, lb, s);
   return launch_status("rv_clahe_median_letterbox_u8");
 }
