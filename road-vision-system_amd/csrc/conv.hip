@@ -1904,6 +1904,13 @@ struct HeadLevels {
 // 16w..16w+15 of the block: box fragments m = 0..REG/4-1, class fragments
 // after them; B fragments are 16-B loads of one anchor's 8 channels, A
 // fragments 16-B loads of the packed [cout][cin_pad32] weights (L2-resident).
+// Class score: exp + one v_rcp_f32 (no IEEE division sequence).  The raw
+// output and the candidate filter use this same function, so the scores NMS
+// sees are the scores in `raw`.
+__device__ __forceinline__ float head_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+
 template <int REG, bool FUSED>
 __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B, int nc,
                                                             float conf, float* __restrict__ raw,
@@ -2052,9 +2059,12 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
       v[i] = __expf(v[i] - mx);
       sum += v[i];
     }
+    // softmax probabilities by one reciprocal (v_rcp_f32, <= 1 ulp from
+    // v / sum; the decode tolerance is 2e-3 px)
+    const float rs = __builtin_amdgcn_rcpf(sum);
     float e = 0.f;
 #pragma unroll
-    for (int i = 0; i < REG; ++i) e += (float)i * (v[i] / sum);
+    for (int i = 0; i < REG; ++i) e += (float)i * (v[i] * rs);
     d = e;
   }
   // classes part, part+4, ...: first maximum of the sigmoid scores
@@ -2062,7 +2072,7 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
   float best = -1.f;
   int bc = 0;
   for (int c = part; c < nc; c += 4) {
-    const float sg = 1.0f / (1.0f + __expf(-pc[c]));
+    const float sg = head_sigmoid(pc[c]);
     if (sg > best) {
       best = sg;
       bc = c;
@@ -2090,7 +2100,7 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
   const float w = (x2 - x1) * L.stride, hh = (y2 - y1) * L.stride;
   if (raw && live) {
     for (int c = part; c < nc; c += 4)
-      raw[((size_t)b * (4 + nc) + 4 + c) * A + a] = 1.0f / (1.0f + __expf(-pc[c]));
+      raw[((size_t)b * (4 + nc) + 4 + c) * A + a] = head_sigmoid(pc[c]);
     const float bxv = part == 0 ? cx : (part == 1 ? cy : (part == 2 ? w : hh));
     raw[((size_t)b * (4 + nc) + part) * A + a] = bxv;
   }
