@@ -20,9 +20,16 @@
 // zero in both operands -- and cv2's 32-channel chunks ascending), the same
 // epilogue (bias, SiLU, residual add of the bf16 input, round to bf16).
 //
-// LDS maps are pixel-major, PB = 2C bytes per pixel (C channels of bf16),
-// 16-B quarters XOR-swizzled by pixel index so the 16 pixels of a fragment
-// hit disjoint bank groups.
+// LDS maps are pixel-major and linear: PB = 2C bytes per pixel (C channels
+// of bf16), quarter q of pixel p at p*PB + 16q.  With the region widths
+// compile-time, every tap of a 3x3 conv is one ds_read_b128 at a constant
+// offset from the lane's base address: no per-tap address VALU (the XOR
+// swizzle this replaced cost ~5 VALU per tap and pair, and the chain loops
+// were VALU-issue-bound).  gfx950 ds_read_b128 lane groups ({0-3,12-15,
+// 20-27}, {4-11,16-19,28-31}, +32): PB = 32 is conflict-free for 16
+// consecutive pixels, PB = 64 at most 2-way.  At C = 16 the k-padding
+// quarters (2, 3) of a B fragment read a zeroed LDS span instead of a
+// branch per tap.
 #include "conv.h"
 
 namespace rv {
@@ -45,11 +52,7 @@ struct C2fGeo {
   static constexpr int PB = 2 * C;      // bytes per pixel
   static constexpr int NQ = PB / 16;    // 16-B quarters per pixel
   static constexpr int MR = C / 16;     // 16-cout fragments of a C-out conv
-  // physical quarter of logical quarter q of pixel p
-  __device__ static __forceinline__ int swz(int p, int q) {
-    return NQ == 4 ? (q ^ ((p >> 2) & 3)) : (q ^ ((p >> 3) & 1));
-  }
-  __device__ static __forceinline__ int addr(int p, int q) { return p * PB + (swz(p, q) << 4); }
+  __device__ static __forceinline__ int addr(int p, int q) { return p * PB + (q << 4); }
 };
 
 template <int TR, int TC>
@@ -69,23 +72,28 @@ struct C2fLds {
   static constexpr int Z0 = Tb + T::rp(h - 1) * G::PB;         // z_0, halo h-2
   static constexpr int Z1 = Z0 + T::rp(h - 2) * G::PB;         // z_1, halo h-4 (N = 2)
   static constexpr int Y0 = Z1 + (N == 2 ? T::rp(0) * G::PB : 0);  // y0, halo 0
-  static constexpr int BYTES = Y0 + T::rp(0) * G::PB;
+  // zeros read by the k-padding quarters at C = 16: the largest tap offset
+  // span (2 rows + 2 pixels of the widest input region) + one quarter
+  static constexpr int ZR = Y0 + T::rp(0) * G::PB;
+  static constexpr int ZBYTES = G::NQ < 4 ? (2 * T::rw(h) + 3) * G::PB : 0;
+  static constexpr int BYTES = ZR + ZBYTES;
 };
 
 // 3x3 C -> C conv from an LDS map at halo e_out + 1 into one at halo e_out
 // (+ residual from an LDS map at halo e_res), zero outside the image.
-template <int C, int TR, int TC, bool RES>
+template <int C, int TR, int TC, bool RES, int EO, int ER>
 __device__ __forceinline__ void c2f_conv3(const uint8_t* __restrict__ in, uint8_t* __restrict__ outb,
-                                          int e_out, const bf16_t* __restrict__ w,
+                                          const bf16_t* __restrict__ w,
                                           const float* __restrict__ bias,
-                                          const uint8_t* __restrict__ res, int e_res, int oy0,
-                                          int ox0, int H, int W) {
+                                          const uint8_t* __restrict__ res, int oy0, int ox0, int H,
+                                          int W, const uint8_t* __restrict__ zeros) {
   using G = C2fGeo<C>;
   using T = C2fTile<TR, TC>;
   constexpr int MR = G::MR;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int col = lane & 15, quad = lane >> 4;
-  const int rwo = T::rw(e_out), rpo = T::rp(e_out), rwi = rwo + 2, rwr = T::rw(e_res);
+  constexpr int e_out = EO, e_res = ER;
+  constexpr int rwo = T::rw(e_out), rpo = T::rp(e_out), rwi = rwo + 2, rwr = T::rw(e_res);
   // A fragments of all 9 taps: packed [Cout_pad16][3][3][32] (Cin zero-padded to 32)
   bf16x8c A[9][MR];
 #pragma unroll
@@ -100,13 +108,14 @@ __device__ __forceinline__ void c2f_conv3(const uint8_t* __restrict__ in, uint8_
   const int nfrag = (rpo + 15) / 16;
   for (int f0 = wave * 2; f0 < nfrag; f0 += 16) {
     f32x4c acc[2][MR];
-    int base[2], o[2];
+    int o[2];
+    const uint8_t* bp[2];  // this lane's quarter of the tap-(0,0) pixel
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
       o[n] = (f0 + n) * 16 + col;
       const int oo = o[n] < rpo ? o[n] : 0;
       const int r = oo / rwo, c = oo - r * rwo;
-      base[n] = r * rwi + c;
+      bp[n] = quad < G::NQ ? in + G::addr(r * rwi + c, quad) : zeros;
 #pragma unroll
       for (int m = 0; m < MR; ++m) acc[n][m] = f32x4c{0.f, 0.f, 0.f, 0.f};
     }
@@ -116,9 +125,7 @@ __device__ __forceinline__ void c2f_conv3(const uint8_t* __restrict__ in, uint8_
       for (int kx = 0; kx < 3; ++kx) {
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
-          const int p = base[n] + ky * rwi + kx;
-          uint4 b = make_uint4(0, 0, 0, 0);
-          if (quad < G::NQ) b = *(const uint4*)(in + G::addr(p, quad));
+          const uint4 b = *(const uint4*)(bp[n] + (ky * rwi + kx) * G::PB);
           const bf16x8c B = __builtin_bit_cast(bf16x8c, b);
 #pragma unroll
           for (int m = 0; m < MR; ++m)
@@ -202,22 +209,24 @@ __global__ __launch_bounds__(512) void c2f_chain_kernel(C2fArgs a) {
       for (int u = 0; u < IT; ++u)
         if (dst[u] >= 0) *(uint4*)(smem + dst[u]) = v[u];
     }
+    for (int i = tid; i < L::ZBYTES / 16; i += 512) *(uint4*)(smem + L::ZR + 16 * i) = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
 
   // ---- 2. bottlenecks: t = cva(y_in) at halo e-1, z = [y_in +] cvb(t) at e-2
-  c2f_conv3<C, TR, TC, false>(smem + L::Y, smem + L::Tb, h - 1, a.wa[0], a.ba[0], nullptr, 0, oy0,
-                              ox0, a.H, a.W);
+  const uint8_t* zeros = smem + L::ZR;
+  c2f_conv3<C, TR, TC, false, h - 1, 0>(smem + L::Y, smem + L::Tb, a.wa[0], a.ba[0], nullptr, oy0,
+                                        ox0, a.H, a.W, zeros);
   __syncthreads();
-  c2f_conv3<C, TR, TC, SC>(smem + L::Tb, smem + L::Z0, h - 2, a.wb[0], a.bb[0], smem + L::Y, h, oy0,
-                           ox0, a.H, a.W);
+  c2f_conv3<C, TR, TC, SC, h - 2, h>(smem + L::Tb, smem + L::Z0, a.wb[0], a.bb[0], smem + L::Y, oy0,
+                                     ox0, a.H, a.W, zeros);
   __syncthreads();
   if constexpr (N == 2) {
-    c2f_conv3<C, TR, TC, false>(smem + L::Z0, smem + L::Tb, h - 3, a.wa[1], a.ba[1], nullptr, 0, oy0,
-                                ox0, a.H, a.W);
+    c2f_conv3<C, TR, TC, false, h - 3, 0>(smem + L::Z0, smem + L::Tb, a.wa[1], a.ba[1], nullptr, oy0,
+                                          ox0, a.H, a.W, zeros);
     __syncthreads();
-    c2f_conv3<C, TR, TC, SC>(smem + L::Tb, smem + L::Z1, h - 4, a.wb[1], a.bb[1], smem + L::Z0, h - 2,
-                             oy0, ox0, a.H, a.W);
+    c2f_conv3<C, TR, TC, SC, h - 4, h - 2>(smem + L::Tb, smem + L::Z1, a.wb[1], a.bb[1],
+                                           smem + L::Z0, oy0, ox0, a.H, a.W, zeros);
     __syncthreads();
   }
 

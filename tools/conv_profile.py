@@ -26,7 +26,8 @@ for _ in range(3):
 if not os.environ.get("NO_TUNE"):
     eng.autotune(lb)
 lib = _lib.load()
-lib.rv_yolo_profile(eng._h, N)
+REPS = int(os.environ.get("REPS", 5))  # launches per event pair (event overhead)
+lib.rv_yolo_profile_reps(eng._h, N, REPS)
 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 torch.cuda.synchronize()
 s.record()
