@@ -353,6 +353,8 @@ class YOLOHip(Detector):
         key = (H, W)
         e = self._engines.get(key)
         if e is None or e.max_batch < max_batch:
+            if e is not None:  # a larger batch replaces it: free its plan first
+                e.close()
             e = YoloEngine(self.variant, self.flat, max_batch, (H, W), imgsz=self.imgsz,
                            conf=self.conf, iou=self.iou, max_det=self.max_det,
                            classes_keep=self.keep, device=self.device)
