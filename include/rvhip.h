@@ -420,6 +420,40 @@ int rv_fog_rain_u8(const uint8_t* in, uint8_t* out, int B, int H, int W, int pit
                    const float* frame_params, const float* grids, int grid_stride,
                    void* ws, size_t ws_bytes, void* stream);
 
+/* The whole EnhancedFogSynthesizer.synthesize (fog.py:227-299) with every
+ * filter, as opencv-python runs it: the image airlight (band luminance
+ * 0.9-quantile, masked mean, tint, filtered gradient map; fog.py:120-139),
+ * the edge-guided transmission (_guided_filter's bilateralFilter fallback,
+ * d 17, sigma 12 / 12; fog.py:55-67,172-179), scattering + global veil,
+ * _glow (fog.py:182-191), _depth_blur (fog.py:194-214),
+ * _local_contrast_fade (fog.py:217-224), tint, gamma, sensor noise, rain.
+ * consts / scene / grids / rain as rv_fog_rain_u8.
+ * full (host, RV_FOG_NFULL f32): {band_h, k, t, edge_guided, 0...}: the
+ *   airlight band rows (max(10, int(0.12 H))) and np.quantile's f32 'linear'
+ *   constants for n = band_h * W (k = floor((n-1)*0.9f), t = remainder).
+ * depth (device f32 H x W): _depth_proxy's clipped depth.
+ * amap_unit (device f32 H x W): the airlight filter applied to vgrad x xgrad
+ *   (the per-channel map is a_c times it; rvs_amd.augment.airlight_unit_map).
+ * bands (device u8 H x W): the _depth_blur band of each pixel (0..2, 3 none).
+ * frame_params (device, B x RV_FOG_NPARAM_FULL f32): {beta, airlight tint
+ *   b/g/r, airlight target mean, tint b/g/r, gamma, rain_seed, glow strength,
+ *   contrast drop, has_noise, band kernel sizes x 3 (0 = skip), glow mask
+ *   kernel k, glow image kernel k2, fade diameter d, 0...}; k, k2, band sizes
+ *   <= 63, d <= 15.
+ * noise (device f32 B x H x W x 3 or NULL): the sensor-noise normals of the
+ *   frames whose has_noise is set.
+ * ws: rv_fog_full_ws_bytes(B, H, W) bytes (56 B per pixel + partials).
+ * H, W >= 64. */
+#define RV_FOG_NPARAM_FULL 24
+#define RV_FOG_NFULL 8
+size_t rv_fog_full_ws_bytes(int B, int H, int W);
+int rv_fog_full_u8(const uint8_t* in, uint8_t* out, int B, int H, int W, int pitch,
+                   const float* consts, int n_consts, const float* full, int n_full,
+                   const float* scene, const float* depth, const float* amap_unit,
+                   const uint8_t* bands, const float* frame_params, const float* grids,
+                   int grid_stride, const float* noise, void* ws, size_t ws_bytes,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,6 +68,11 @@ _SIGS = {
     "rv_fog_rain_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_size_t,
                                c_void_p]),
+    "rv_fog_full_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "rv_fog_full_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                               c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_size_t,
+                               c_void_p]),
     "rv_letterbox_geometry": (c_int, [c_int, c_int, c_int, c_int, POINTER(c_int)]),
     "rv_letterbox_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                 POINTER(c_int), c_void_p]),

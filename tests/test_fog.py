@@ -14,6 +14,7 @@ from oracle import fog_ref
 
 def _synth(**kw):
     from rvs_amd.augment import FogSynthesizer
+    kw.setdefault("filters", False)
     return FogSynthesizer(device="cpu", **kw)
 
 
@@ -99,3 +100,143 @@ def test_abi_argument_errors():
                               None) == -1000
     assert lib.rv_fog_rain_u8(p, ctypes.c_void_p(32), 1, 8, 8, 24, c, 26, p, p, p, 4, p, ws,
                               None) == -1000  # n_oct = 0
+
+
+# --- full synthesize (rv_fog_full_u8): host logic and the oracle's pieces ---
+
+@pytest.mark.parametrize("kw", [dict(), dict(level="heavy", rain_p=0.01), dict(mor=150.0)])
+def test_full_draw_matches_oracle(kw):
+    """The full path's draw keeps every value of fog.py's draw order (airlight
+    tint, target mean, glow, contrast drop, the sensor-noise normals) and
+    derives the filter sizes exactly as fog.py does."""
+    from rvs_amd.augment import FogSynthesizer, band_radii
+    h, w = 72, 120
+    syn = FogSynthesizer(device="cpu", seed=9, filters=True, **kw)
+    rng = np.random.RandomState(9)
+    fired = 0
+    for _ in range(6):
+        p, g, nz = syn.draw(h, w)
+        r = fog_ref.draw_full(rng, h, w, level=kw.get("level", "medium"), mor=kw.get("mor"),
+                              rain=kw.get("rain_p", 0) > 0)
+        assert p[0] == np.float32(r["beta"]) and p[4] == np.float32(r["a_target"])
+        np.testing.assert_array_equal(p[1:4], r["tint_a"])
+        np.testing.assert_array_equal(p[5:8], r["tint"])
+        assert p[8] == np.float32(r["gamma"]) and int(p[9]) == r["rain_seed"]
+        assert p[10] == np.float32(r["glow"]) and p[11] == np.float32(r["cdrop"])
+        np.testing.assert_array_equal(g, np.concatenate([x.ravel() for x in r["grids"]]))
+        assert (nz is None) == (r["noise"] is None) and p[12] == (nz is not None)
+        if nz is not None:
+            fired += 1
+            np.testing.assert_array_equal(nz, r["noise"])
+        assert p[16] == (int(9 + 20 * r["glow"]) | 1)
+        assert p[17] == (int(max(7, (h + w) * (0.003 + 0.01 * r["glow"]))) | 1)
+        assert p[18] == (int(5 + r["cdrop"] * 20) | 1)
+        depth, _ = fog_ref.depth_and_sky(h, w)
+        want = {rad: True for _, rad in fog_ref.depth_bands(depth, r["beta"], 3.5)}
+        got = [int(v) for v in p[13:16] if v > 0]
+        assert sorted(got) == sorted(want)
+    assert fired > 0 or kw
+
+
+def test_full_scene_maps_match_oracle():
+    """Per-resolution maps of the full path: the depth map and the depth-band
+    masks equal the oracle's _depth_proxy / _depth_blur bands bit for bit; the
+    airlight unit map scaled by a channel's sky colour equals the literal
+    bilateral restatement of the A_map filter (fog.py:136-138) to < 1e-5."""
+    from rvs_amd.augment import airlight_unit_map, depth_band_map, fog_depth
+    for h, w in ((96, 160), (135, 240)):
+        depth = fog_depth(h, w)
+        ref, _ = fog_ref.depth_and_sky(h, w)
+        np.testing.assert_array_equal(depth, ref)
+        bands = depth_band_map(depth)
+        prev = np.zeros_like(ref)
+        for i, b in enumerate((0.33, 0.66, 1.0)):
+            np.testing.assert_array_equal(bands == i, (ref >= prev) & (ref < b))
+            prev = np.full_like(ref, b)
+        unit = airlight_unit_map(h, w)
+        a = np.array([0.93, 0.86, 0.99], np.float32)
+        amap = (np.linspace(1.0, 0.85, h, dtype=np.float32)[:, None, None] * a[None, None, :] *
+                np.linspace(0.95, 1.05, w, dtype=np.float32)[None, :, None])
+        for c in range(3):
+            lit = fog_ref.bilateral_f32(amap[:, :, c], 33, 12, 12)
+            assert np.abs(lit - a[c] * unit).max() < 1e-5
+
+
+def test_quantile_constants_reproduce_numpy():
+    """np.quantile(lum, 0.9) of an f32 array: q cast to f32, f32 virtual index
+    and lerp (the device's radix select + lerp use these constants)."""
+    from rvs_amd.augment import quantile_consts
+    rng = np.random.default_rng(0)
+    for n in list(rng.integers(2, 4000, 60)) + [19200, 248320]:
+        n = int(n)
+        a = (rng.integers(0, 256, n) / np.float32(255) * np.float32(0.587) +
+             rng.integers(0, 256, n) / np.float32(255) * np.float32(0.114)).astype(np.float32)
+        s = np.sort(a)
+        k, t = quantile_consts(n)
+        t = np.float32(t)
+        lo, hi = s[k], s[min(k + 1, n - 1)]
+        d = np.float32(hi - lo)
+        v = np.float32(lo + d * t) if t < 0.5 else np.float32(hi - d * (np.float32(1) - t))
+        assert v == np.quantile(a, 0.9)
+
+
+def test_opencv_filter_restatements():
+    """The oracle's OpenCV restatements against independent forms: the
+    separable Gaussian against scipy.ndimage.correlate (mode 'mirror' =
+    BORDER_REFLECT_101), both bilaterals against brute-force per-pixel loops,
+    addWeighted's rounding, and the Gaussian kernel's normalisation."""
+    from scipy import ndimage
+    rng = np.random.default_rng(1)
+    img = rng.random((23, 31)).astype(np.float32)
+    for k, sig in ((5, 1.75), (13, 4.55), (17, 4.25)):
+        kern = fog_ref.gaussian_kernel(k, sig)
+        assert abs(float(kern.astype(np.float64).sum()) - 1.0) < 1e-6
+        want = ndimage.correlate(img.astype(np.float64), np.outer(kern, kern), mode="mirror")
+        np.testing.assert_allclose(fog_ref.gaussian_blur(img, k, sig), want, atol=2e-6)
+    small = rng.random((9, 11)).astype(np.float32)
+    got = fog_ref.bilateral_f32(small, 5, 0.3, 2.0)
+    h, w = small.shape
+    mn, mx = float(small.min()), float(small.max())
+    for y in range(h):
+        for x in range(w):
+            s = ws = 0.0
+            for i in range(-2, 3):
+                for j in range(-2, 3):
+                    if i * i + j * j > 4:
+                        continue
+                    v = float(small[fog_ref.reflect101(y + i, h), fog_ref.reflect101(x + j, w)])
+                    wt = np.exp(-(i * i + j * j) / 8.0) * np.exp(-((v - small[y, x]) ** 2) / 0.18)
+                    s, ws = s + v * wt, ws + wt
+            assert abs(got[y, x] - s / ws) < 2e-4 * (mx - mn)
+    u8 = rng.integers(0, 256, (10, 12)).astype(np.uint8)
+    got = fog_ref.bilateral_u8(u8, 5, 30.0, 30.0)
+    for y in range(10):
+        for x in range(12):
+            s = ws = 0.0
+            for i in range(-2, 3):
+                for j in range(-2, 3):
+                    if i * i + j * j > 4:
+                        continue
+                    v = int(u8[fog_ref.reflect101(y + i, 10), fog_ref.reflect101(x + j, 12)])
+                    wt = np.exp(-(i * i + j * j) / 1800.0) * np.exp(-((v - int(u8[y, x])) ** 2)
+                                                                   / 1800.0)
+                    s, ws = s + v * wt, ws + wt
+            assert abs(int(got[y, x]) - s / ws) <= 0.5 + 1e-3
+    a, b = np.array([10, 200, 255], np.uint8), np.array([20, 100, 0], np.uint8)
+    np.testing.assert_array_equal(fog_ref.add_weighted_u8(a, 0.75, b, 0.25), [12, 175, 191])
+
+
+def test_full_abi_argument_errors():
+    from rvs_amd import _lib
+    lib = _lib.load()
+    c = (ctypes.c_float * 26)()
+    fl = (ctypes.c_float * 8)()
+    p = ctypes.c_void_p(16)
+    assert lib.rv_fog_full_u8(None, None, 1, 64, 64, 192, c, 26, fl, 8, p, p, p, p, p, p, 4,
+                              None, p, 0, None) == -1000
+    assert b"null" in lib.rv_last_error()
+    # frames below the separable filters' 64-pixel minimum are refused
+    assert lib.rv_fog_full_u8(p, ctypes.c_void_p(32), 1, 32, 64, 192, c, 26, fl, 8, p, p, p, p,
+                              p, p, 4, None, p, 1 << 30, None) == -1000
+    assert lib.rv_fog_full_ws_bytes(2, 64, 64) >= 2 * 64 * 64 * 56
+    assert lib.rv_fog_full_ws_bytes(0, 64, 64) == 0
