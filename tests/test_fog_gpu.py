@@ -63,14 +63,15 @@ def test_fog_single_frame_api_and_batch_consistency(cuda):
 # colour weight (numpy: the 4096-bin LUT), the airlight map's filter from the
 # rank-1 form (< 1e-5), and two truncations to u8 on the way (the glow's
 # gray plane and the contrast fade's YCrCb) that turn an ulp into a step.
-# Bar: |d| <= 2 and >= 98 % of channel values exact.
+# Bar: |d| <= 2 and >= 99.9 % of channel values exact (measured r02: all
+# frames exact but one, 2e-5 of its values off by 2).
 
 def _check_full(got, ref):
     d = np.abs(got.astype(np.int16) - ref.astype(np.int16))
     exact = float((d == 0).mean())
     print(f"full fog: max |d| {d.max()}, exact {exact:.5f}, |d|>1 {(d > 1).mean():.2e}")
     assert d.max() <= 2, f"max |d| {d.max()}"
-    assert exact >= 0.98, f"exact fraction {exact:.4f}"
+    assert exact >= 0.999, f"exact fraction {exact:.4f}"
 
 
 @pytest.mark.parametrize("H,W,B,kw", [

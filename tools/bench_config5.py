@@ -1,8 +1,9 @@
 """BASELINE config 5 (configs[4]): "YOLOv8m 1280x1280 fp8 MFMA conv path,
 batch=16, fog/rain-augmented frames (tools/fog_batch)".
 
-A step = fog/rain synthesis on the device (rv_fog_rain_u8, from clean frames
-resident in HBM) -> letterbox -> YOLOv8m forward at imgsz 1280 -> NMS, for a
+A step = fog/rain synthesis on the device (rv_fog_full_u8 with
+tools/fog_batch.py's settings, or the one-pass core rv_fog_rain_u8 with
+--fog core; from clean frames resident in HBM) -> letterbox -> YOLOv8m forward at imgsz 1280 -> NMS, for a
 batch of 16.  --dtype fp8 (default) runs the conv stack on
 v_mfma_f32_16x16x32_fp8_fp8 with e4m3 weights / activations (scales
 calibrated once on the first batch), bf16 the bf16 plan.
@@ -39,6 +40,9 @@ def parse():
     p.add_argument("--autotune", type=int, default=1)
     p.add_argument("--cpu-frames", type=int, default=16, help="0 skips the CPU baseline")
     p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--fog", default="full", choices=["full", "core"],
+                   help="full: the reference's whole synthesize with tools/fog_batch.py's "
+                        "settings (rv_fog_full_u8); core: the one-pass scattering core")
     return p.parse_args()
 
 
@@ -84,7 +88,8 @@ def cpu_baseline(clean_host, flat, frames, threads):
     return {"value": round(frames / dt, 4), "unit": "frames/s", "cores": threads, "kind": "port",
             "host_cpus": os.cpu_count(), "stage_s_per_frame": {
                 k: round(v / frames, 3) for k, v in zip(["fog+letterbox", "yolov8m_fp32", "nms"], t)},
-            "sample": f"{frames} frame(s) of 1280x1280: oracle fog_frame (numpy f32) + torch-CPU "
+            "sample": f"{frames} frame(s) of 1280x1280: oracle fog_frame (numpy f32, the scattering "
+                      f"core; the full filter chain is not timed on the CPU) + torch-CPU "
                       f"fp32 YOLOv8m ({threads} threads) + restated NMS; {dt:.1f} s"}
 
 
@@ -98,7 +103,12 @@ def main():
     dev = torch.device("cuda:0")
     clean_host = np.stack([road_frame(H, W, seed=70 + b) for b in range(4)])
     clean = torch.from_numpy(clean_host).to(dev).repeat((B + 3) // 4, 1, 1, 1)[:B].contiguous()
-    syn = FogSynthesizer(level="medium", seed=5, rain_p=0.002, device=dev)
+    if args.fog == "full":  # tools/fog_batch.py:20-28
+        syn = FogSynthesizer(level="medium", seed=5, rain_p=0.002, device=dev, y_h_ratio=0.42,
+                             perlin_scale_ratio=0.18, perlin_octaves=2, horizon_softness=0.07,
+                             global_veil=0.5, depth_blur_max=4.0)
+    else:
+        syn = FogSynthesizer(level="medium", seed=5, rain_p=0.002, device=dev, filters=False)
     prep = syn.prepare([syn.draw(H, W) for _ in range(B)])
     fog = syn.synthesize_batch(clean, prepared=prep)
     flat = weights.synthetic_weights(2, seed=0)
@@ -145,7 +155,7 @@ def main():
         "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (road frames + device fog/rain; "
         "synthetic YOLOv8m weights)",
         "config": {"workload": f"configs[4]: YOLOv8m 1280x1280 {args.dtype} conv path, batch {B}, "
-                               "fog/rain frames", "batch": B, "imgsz": 1280,
+                               "fog/rain frames", "batch": B, "imgsz": 1280, "fog": args.fog,
                    "autotune": bool(args.autotune)},
         "stage_ms": {"fog": round(ms_fog, 4), "forward": round(ms_fwd, 4), "nms": round(ms_nms, 4)},
         "roofline": {
