@@ -302,7 +302,9 @@ __global__ __launch_bounds__(256) void fog_apply_kernel(
 
 constexpr int kSepRMax = 31;   // Gaussian kernels up to 63 taps
 constexpr int kFadeRMax = 7;   // contrast-fade bilateral up to d = 15
-constexpr int kAirThreads = 1024;
+// per-frame filter table offsets (floats; fog_taps_kernel)
+constexpr int kTabGlowA = 0, kTabGlowB = 32, kTabBand = 64, kTabCw = 160, kTabSw = 416,
+              kTabTbil = 480, kTabStride = 576;
 
 struct FogFull {
   int band_h, q_k, edge_guided, nblk;
@@ -328,101 +330,163 @@ __device__ double block_sum_f64(double v, double* red) {
   return s;
 }
 
-// One workgroup per frame.  k-th smallest band luminance by a 3-pass radix
-// select on the f32 bit patterns (non-negative floats order as integers),
-// the (k+1)-th, numpy's f32 lerp, then the per-channel mean of the band
-// pixels at or above the threshold (all of them if fewer than 100).
-__global__ __launch_bounds__(kAirThreads) void fog_air_kernel(
-    const uint8_t* __restrict__ in, int W, int pitch, size_t fstride, FogFull f,
-    const float* __restrict__ fparams, float* __restrict__ air) {
-  __shared__ uint32_t hist[2048];
-  __shared__ uint32_t s_pref, s_mask, s_k, s_eq, s_min;
-  __shared__ double red[16];
-  const int b = blockIdx.x;
+// Image airlight (fog.py:120-130) over all frames' bands at once: the k-th
+// smallest band luminance by a 3-pass radix select on the f32 bit patterns
+// (non-negative floats order as integers; 11 / 11 / 10 bits), the (k+1)-th
+// as the minimum key above it, numpy's f32 lerp, then the per-channel mean
+// of the band pixels at or above the threshold (all of them if fewer than
+// 100).  Workgroups keep LDS histograms and flush their non-zero bins.
+struct AirState {
+  uint32_t pref, mask, k, eq, min_gt, pad[3];
+  double sum[12];  // gt b/g/r/count, eq b/g/r/count, all b/g/r, 0
+};
+constexpr int kAirPerBlock = 2048;
+
+__global__ __launch_bounds__(256) void fog_lum_kernel(const uint8_t* __restrict__ in, int W,
+                                                      int pitch, size_t fstride, int n,
+                                                      uint32_t* __restrict__ keys,
+                                                      uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[2048];
+  const int b = blockIdx.y;
+  for (int i = threadIdx.x; i < 2048; i += 256) h[i] = 0;
+  __syncthreads();
   const uint8_t* src = in + (size_t)b * fstride;
-  const int n = f.band_h * W;
+  const int i0 = blockIdx.x * kAirPerBlock;
+  for (int i = i0 + threadIdx.x; i < min(n, i0 + kAirPerBlock); i += 256) {
+    const int y = i / W, x = i - y * W;
+    const uint32_t key = __float_as_uint(band_lum(src + (size_t)y * pitch + 3 * x));
+    keys[(size_t)b * n + i] = key;
+    atomicAdd(&h[key >> 21], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2048; i += 256)
+    if (h[i]) atomicAdd(&hist[(size_t)b * 2048 + i], h[i]);
+}
+
+__global__ __launch_bounds__(256) void fog_hist_kernel(const uint32_t* __restrict__ keys, int n,
+                                                       int shift, int nb,
+                                                       const AirState* __restrict__ st,
+                                                       uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[2048];
+  const int b = blockIdx.y;
+  for (int i = threadIdx.x; i < nb; i += 256) h[i] = 0;
+  __syncthreads();
+  const uint32_t pref = st[b].pref, msk = st[b].mask;
+  const int i0 = blockIdx.x * kAirPerBlock;
+  for (int i = i0 + threadIdx.x; i < min(n, i0 + kAirPerBlock); i += 256) {
+    const uint32_t key = keys[(size_t)b * n + i];
+    if ((key & msk) == pref) atomicAdd(&h[(key >> shift) & (nb - 1)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += 256)
+    if (h[i]) atomicAdd(&hist[(size_t)b * 2048 + i], h[i]);
+}
+
+// One workgroup per frame: the bin holding the k-th key; clears the
+// histogram for the next pass.
+__global__ __launch_bounds__(256) void fog_sel_kernel(uint32_t* __restrict__ hist, int shift,
+                                                      int nb, int first, int q_k,
+                                                      AirState* __restrict__ st) {
+  __shared__ uint32_t part[256];
+  const int b = blockIdx.x;
+  uint32_t* hb = hist + (size_t)b * 2048;
+  const int per = nb / 256;
+  uint32_t v = 0;
+  for (int i = 0; i < per; ++i) v += hb[threadIdx.x * per + i];
+  part[threadIdx.x] = v;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    s_pref = 0;
-    s_mask = 0;
-    s_k = (uint32_t)f.q_k;
-    s_min = 0xffffffffu;
-  }
-  const int shifts[3] = {21, 10, 0}, bits[3] = {11, 11, 10};
-  for (int ps = 0; ps < 3; ++ps) {
-    const int nb = 1 << bits[ps];
-    for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0;
-    __syncthreads();
-    const uint32_t pref = s_pref, msk = s_mask;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-      const int y = i / W, x = i - y * W;
-      const uint32_t key = __float_as_uint(band_lum(src + (size_t)y * pitch + 3 * x));
-      if ((key & msk) == pref) atomicAdd(&hist[(key >> shifts[ps]) & (nb - 1)], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t cum = 0, k = s_k;
-      int bin = nb - 1;
-      for (int i = 0; i < nb; ++i) {
-        if (cum + hist[i] > k) {
-          bin = i;
-          break;
-        }
-        cum += hist[i];
+    const uint32_t k = first ? (uint32_t)q_k : st[b].k;
+    uint32_t cum = 0;
+    int t = 255;
+    for (int i = 0; i < 256; ++i) {
+      if (cum + part[i] > k) {
+        t = i;
+        break;
       }
-      s_k = k - cum;
-      s_eq = hist[bin];
-      s_pref = pref | ((uint32_t)bin << shifts[ps]);
-      s_mask = msk | ((uint32_t)(nb - 1) << shifts[ps]);
+      cum += part[i];
     }
-    __syncthreads();
-  }
-  const uint32_t lo = s_pref;
-  const bool same = s_k + 1 < s_eq || f.q_k + 1 >= n;
-  if (!same) {
-    uint32_t m = 0xffffffffu;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-      const int y = i / W, x = i - y * W;
-      const uint32_t key = __float_as_uint(band_lum(src + (size_t)y * pitch + 3 * x));
-      if (key > lo) m = min(m, key);
+    int bin = t * per + per - 1;
+    for (int i = t * per; i < t * per + per; ++i) {
+      if (cum + hb[i] > k) {
+        bin = i;
+        break;
+      }
+      cum += hb[i];
     }
-    atomicMin(&s_min, m);
-    __syncthreads();
+    const uint32_t pref = first ? 0u : st[b].pref, msk = first ? 0u : st[b].mask;
+    st[b].k = k - cum;
+    st[b].eq = hb[bin];
+    st[b].pref = pref | ((uint32_t)bin << shift);
+    st[b].mask = msk | ((uint32_t)(nb - 1) << shift);
+    if (first) st[b].min_gt = 0xffffffffu;
   }
-  const float a = __uint_as_float(lo), bq = same ? a : __uint_as_float(s_min);
-  const float d = __fsub_rn(bq, a);
-  const float thr = f.q_t >= 0.5f ? __fsub_rn(bq, __fmul_rn(d, __fsub_rn(1.f, f.q_t)))
-                                  : __fadd_rn(a, __fmul_rn(d, f.q_t));
-  double sb = 0, sg = 0, sr = 0, tb = 0, tg = 0, tr = 0, cnt = 0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += 256) hb[i] = 0;
+}
+
+__global__ __launch_bounds__(256) void fog_airsum_kernel(const uint8_t* __restrict__ in, int W,
+                                                         int pitch, size_t fstride, int n,
+                                                         const uint32_t* __restrict__ keys,
+                                                         AirState* __restrict__ st) {
+  __shared__ double red[4];
+  __shared__ uint32_t s_min;
+  const int b = blockIdx.y;
+  const uint32_t lo = st[b].pref;
+  if (threadIdx.x == 0) s_min = 0xffffffffu;
+  double a[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t mgt = 0xffffffffu;
+  const uint8_t* src = in + (size_t)b * fstride;
+  const int i0 = blockIdx.x * kAirPerBlock;
+  for (int i = i0 + threadIdx.x; i < min(n, i0 + kAirPerBlock); i += 256) {
     const int y = i / W, x = i - y * W;
     const uint8_t* p = src + (size_t)y * pitch + 3 * x;
     const float vb = u8f(p[0]), vg = u8f(p[1]), vr = u8f(p[2]);
-    tb += vb;
-    tg += vg;
-    tr += vr;
-    if (band_lum(p) >= thr) {
-      sb += vb;
-      sg += vg;
-      sr += vr;
-      cnt += 1.0;
+    const uint32_t key = keys[(size_t)b * n + i];
+    const int o = key > lo ? 0 : (key == lo ? 4 : -1);
+    if (o >= 0) {
+      a[o] += vb;
+      a[o + 1] += vg;
+      a[o + 2] += vr;
+      a[o + 3] += 1.0;
     }
+    if (key > lo) mgt = min(mgt, key);
+    a[8] += vb;
+    a[9] += vg;
+    a[10] += vr;
   }
-  cnt = block_sum_f64(cnt, red);
-  sb = block_sum_f64(sb, red);
-  sg = block_sum_f64(sg, red);
-  sr = block_sum_f64(sr, red);
-  tb = block_sum_f64(tb, red);
-  tg = block_sum_f64(tg, red);
-  tr = block_sum_f64(tr, red);
-  if (threadIdx.x == 0) {
-    const bool all = cnt < 100.0;
-    const double nn = all ? (double)n : cnt;
-    const float m[3] = {(float)((all ? tb : sb) / nn), (float)((all ? tg : sg) / nn),
-                        (float)((all ? tr : sr) / nn)};
-    const float* fp = fparams + (size_t)b * RV_FOG_NPARAM_FULL;
-    for (int c = 0; c < 3; ++c) air[4 * b + c] = fminf(fmaxf(m[c] + fp[1 + c], 0.7f), 1.f);
-    air[4 * b + 3] = thr;
+  __syncthreads();
+  atomicMin(&s_min, mgt);
+  for (int k = 0; k < 11; ++k) {
+    const double v = block_sum_f64(a[k], red);
+    if (threadIdx.x == 0 && v != 0.0) atomicAdd(&st[b].sum[k], v);
   }
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMin(&st[b].min_gt, s_min);
+}
+
+__global__ void fog_airfin_kernel(const AirState* __restrict__ st, FogFull f, int n,
+                                  const float* __restrict__ fparams, float* __restrict__ air) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= (int)gridDim.x * (int)blockDim.x) return;
+  const AirState& s = st[b];
+  const bool same = s.k + 1 < s.eq || f.q_k + 1 >= n;
+  const float a = __uint_as_float(s.pref), bq = same ? a : __uint_as_float(s.min_gt);
+  const float d = __fsub_rn(bq, a);
+  const float thr = f.q_t >= 0.5f ? __fsub_rn(bq, __fmul_rn(d, __fsub_rn(1.f, f.q_t)))
+                                  : __fadd_rn(a, __fmul_rn(d, f.q_t));
+  // mask = lum >= thr: keys above lo, plus those equal to lo when thr == lo
+  const bool with_eq = thr <= a;
+  double m[4];
+  for (int c = 0; c < 4; ++c) m[c] = s.sum[c] + (with_eq ? s.sum[4 + c] : 0.0);
+  const bool all = m[3] < 100.0;
+  const double nn = all ? (double)n : m[3];
+  const float* fp = fparams + (size_t)b * RV_FOG_NPARAM_FULL;
+  for (int c = 0; c < 3; ++c) {
+    const float mean = (float)((all ? s.sum[8 + c] : m[c]) / nn);
+    air[4 * b + c] = fminf(fmaxf(mean + fp[1 + c], 0.7f), 1.f);
+  }
+  air[4 * b + 3] = thr;
 }
 
 // t0 and the airlight-map mean partials.
@@ -496,12 +560,17 @@ __global__ __launch_bounds__(256) void fog_sum_finish(const double* __restrict__
 }
 
 // bilateralFilter(t0, d = 17, 12, 12), BORDER_REFLECT_101; 64 x 16 outputs
-// per workgroup, the tile + radius-8 halo in LDS.  Tap order and the
-// (sum + centre) / (wsum + 1) form follow bilateralFilterInvoker_32f; the
-// colour weight is exp() itself rather than its 4096-bin interpolated LUT
-// (interpolation error < 1e-10 at this range).
+// per workgroup, the tile + radius-8 halo in LDS, two horizontally adjacent
+// outputs per lane as packed f32 pairs (v_pk_mul / v_pk_add / v_pk_fma).
+// Tap order and the (sum + centre) / (wsum + 1) form follow
+// bilateralFilterInvoker_32f.  The colour weight exp(-d^2 / 288), d <= 0.95
+// (t in [0.05, 1]), is 1 + x + x^2 / 2 (x = -d^2 / 288 >= -0.0032: the
+// dropped x^3 / 6 is < 6e-9, under half an f32 ulp of 1), which OpenCV
+// approximates by its 4096-bin interpolated LUT instead.
 constexpr int kTbR = 8, kTbW = 64, kTbH = 16;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void fog_tbil_kernel(const float* __restrict__ t0, int H, int W,
+                                                       const float* __restrict__ tab,
                                                        float* __restrict__ tf) {
   __shared__ float tile[kTbH + 2 * kTbR][kTbW + 2 * kTbR];
   __shared__ float sw[kTbR * kTbR + 1];
@@ -513,27 +582,33 @@ __global__ __launch_bounds__(256) void fog_tbil_kernel(const float* __restrict__
     const int yy = reflect101(y0 + ty - kTbR, H), xx = reflect101(x0 + tx - kTbR, W);
     tile[ty][tx] = src[(size_t)yy * W + xx];
   }
-  if (threadIdx.x <= kTbR * kTbR)
-    sw[threadIdx.x] = (float)exp((double)threadIdx.x * (-0.5 / (12.0 * 12.0)));
+  if (threadIdx.x <= kTbR * kTbR) sw[threadIdx.x] = tab[kTabTbil + threadIdx.x];
   __syncthreads();
-  const float cc = (float)(-0.5 / (12.0 * 12.0)) * 1.44269504088896341f;
-  const int tx = threadIdx.x & 63;
-  for (int r = threadIdx.x >> 6; r < kTbH; r += 4) {
+  const f32x2 cc = (f32x2)(-1.f / 288.f), half = (f32x2)(0.5f), one = (f32x2)(1.f);
+  const int tx = 2 * (threadIdx.x & 31);
+  for (int r = threadIdx.x >> 5; r < kTbH; r += 8) {
     const int y = y0 + r, x = x0 + tx;
     if (y >= H || x >= W) continue;
-    const float c0 = tile[r + kTbR][tx + kTbR];
-    float s = 0.f, ws = 0.f;
+    const f32x2 c0 = {tile[r + kTbR][tx + kTbR], tile[r + kTbR][tx + kTbR + 1]};
+    f32x2 s = (f32x2)(0.f), ws = (f32x2)(0.f);
+#pragma unroll
     for (int i = -kTbR; i <= kTbR; ++i)
+#pragma unroll
       for (int j = -kTbR; j <= kTbR; ++j) {
         const int r2 = i * i + j * j;
         if (r2 > kTbR * kTbR || r2 == 0) continue;
-        const float v = tile[r + kTbR + i][tx + kTbR + j];
-        const float dd = v - c0;
-        const float w = sw[r2] * __builtin_amdgcn_exp2f(dd * dd * cc);
+        const f32x2 v = {tile[r + kTbR + i][tx + kTbR + j], tile[r + kTbR + i][tx + kTbR + j + 1]};
+        const f32x2 dd = v - c0;
+        const f32x2 xx = dd * dd * cc;
+        const f32x2 wc = __builtin_elementwise_fma(__builtin_elementwise_fma(half, xx, one), xx, one);
+        const f32x2 w = (f32x2)(sw[r2]) * wc;
         ws = ws + w;
         s = s + v * w;
       }
-    tf[(size_t)b * H * W + (size_t)y * W + x] = fminf(fmaxf((s + c0) / (ws + 1.f), 0.05f), 1.f);
+    const f32x2 res = (s + c0) / (ws + one);
+    float* d = tf + (size_t)b * H * W + (size_t)y * W + x;
+    d[0] = fminf(fmaxf(res.x, 0.05f), 1.f);
+    if (x + 1 < W) d[1] = fminf(fmaxf(res.y, 0.05f), 1.f);
   }
 }
 
@@ -580,11 +655,15 @@ __global__ __launch_bounds__(256) void fog_scatter_kernel(
   }
 }
 
-// getGaussianKernel(k, sigma, CV_32F): double exp / sum, cast to f32.
-// Writes the centre and right half (r + 1 entries) into kern.
-__device__ void gauss_half(int k, double sigma, float* kern) {
+// Per-frame filter tables (one workgroup per frame, computed once):
+//   getGaussianKernel(k, sigma, CV_32F) half kernels (centre + right half;
+//   double exp / sum, cast to f32) for the glow image (k2, 0.25 k2), the glow
+//   mask (k, 0.35 k) and the three depth bands (rad, 0.5 rad); the contrast
+//   fade's 8U bilateral colour weights (256) and space weights (by r^2); the
+//   transmission bilateral's space weights (by r^2, sigma 12).
+__device__ void gauss_table(int k, double sigma, float* out) {
   __shared__ double tmp[2 * kSepRMax + 1];
-  __shared__ double ssum;
+  __shared__ double inv;
   const int r = k / 2;
   __syncthreads();
   if ((int)threadIdx.x < k) {
@@ -593,13 +672,34 @@ __device__ void gauss_half(int k, double sigma, float* kern) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double s = 0.0;
-    for (int i = 0; i < k; ++i) s += tmp[i];
-    ssum = 1.0 / s;
+    double sum = 0.0;
+    for (int i = 0; i < k; ++i) sum += tmp[i];
+    inv = 1.0 / sum;
   }
   __syncthreads();
-  if ((int)threadIdx.x <= r) kern[threadIdx.x] = (float)(tmp[r + threadIdx.x] * ssum);
-  __syncthreads();
+  if ((int)threadIdx.x <= kSepRMax)
+    out[threadIdx.x] = (int)threadIdx.x <= r ? (float)(tmp[r + threadIdx.x] * inv) : 0.f;
+}
+
+__global__ __launch_bounds__(256) void fog_taps_kernel(const float* __restrict__ fparams,
+                                                       float* __restrict__ tab) {
+  const int b = blockIdx.x;
+  const float* fp = fparams + (size_t)b * RV_FOG_NPARAM_FULL;
+  float* t = tab + (size_t)b * kTabStride;
+  const int k2 = min((int)fp[17], 2 * kSepRMax + 1), k = min((int)fp[16], 2 * kSepRMax + 1);
+  gauss_table(k2, k2 * 0.25, t + kTabGlowA);
+  gauss_table(k, k * 0.35, t + kTabGlowB);
+  for (int i = 0; i < 3; ++i) {
+    const int rad = min(max((int)fp[13 + i], 1), 2 * kSepRMax + 1);
+    gauss_table(rad, rad * 0.5, t + kTabBand + 32 * i);
+  }
+  const double sig = 25.0 + (double)fp[11] * 50.0;
+  const double coef = -0.5 / (sig * sig);
+  t[kTabCw + threadIdx.x] = (float)exp((double)threadIdx.x * threadIdx.x * coef);
+  if (threadIdx.x <= kFadeRMax * kFadeRMax)
+    t[kTabSw + threadIdx.x] = (float)exp((double)threadIdx.x * coef);
+  if (threadIdx.x <= 64)
+    t[kTabTbil + threadIdx.x] = (float)exp((double)threadIdx.x * (-0.5 / (12.0 * 12.0)));
 }
 
 enum { kSepGlow = 0, kSepBand = 1 };
@@ -626,6 +726,7 @@ __device__ __forceinline__ void sep_sizes(int mode, int band, const float* fp, i
 template <int MODE>
 __global__ __launch_bounds__(256) void fog_sep_h(const float4* __restrict__ src, int H, int W,
                                                  const float* __restrict__ fparams,
+                                                 const float* __restrict__ tab,
                                                  const float* __restrict__ thr,
                                                  const uint8_t* __restrict__ bands, int band,
                                                  float4* __restrict__ dst) {
@@ -637,8 +738,15 @@ __global__ __launch_bounds__(256) void fog_sep_h(const float4* __restrict__ src,
   double sa, sb;
   sep_sizes(MODE, band, fp, ka, sa, kb, sb);
   if (MODE == kSepBand && ka <= 1) return;
-  gauss_half(ka, sa, kA);
-  gauss_half(kb, sb, kB);
+  {
+    const float* tb = tab + (size_t)b * kTabStride;
+    const int oa = MODE == kSepGlow ? kTabGlowA : kTabBand + 32 * band;
+    const int ob = MODE == kSepGlow ? kTabGlowB : kTabBand + 32 * band;
+    if (threadIdx.x <= kSepRMax) {
+      kA[threadIdx.x] = tb[oa + threadIdx.x];
+      kB[threadIdx.x] = tb[ob + threadIdx.x];
+    }
+  }
   const int ra = ka / 2, rb = kb / 2, R = max(ra, rb);
   const float4* s = src + (size_t)b * H * W + (size_t)y * W;
   const float th = MODE == kSepGlow ? thr[b] : 0.f;
@@ -669,14 +777,15 @@ __global__ __launch_bounds__(256) void fog_sep_h(const float4* __restrict__ src,
   dst[(size_t)b * H * W + (size_t)y * W + x] = o;
 }
 
-// Column pass + composite.  32 columns x 64 rows per workgroup, the column
+// Column pass + composite.  32 columns x 32 rows per workgroup, the column
 // strip + halo in LDS.  GLOW: soft = clip(blur(mask)), H2 = H1 (in-place
 // copy too) = clip(h (1 - soft) + (h + s blur) soft); BAND: H1 = H1 (1 - m)
 // + blur m.
-constexpr int kVCols = 32, kVRows = 64;
+constexpr int kVCols = 32, kVRows = 32;
 template <int MODE>
 __global__ __launch_bounds__(256) void fog_sep_v(const float4* __restrict__ tmp, int H, int W,
-                                                 const float* __restrict__ fparams, int band,
+                                                 const float* __restrict__ fparams,
+                                                 const float* __restrict__ tab, int band,
                                                  float4* __restrict__ h1, float4* __restrict__ h2) {
   extern __shared__ float4 col[];  // [(kVRows + 2 R) * kVCols]
   __shared__ float kA[kSepRMax + 1], kB[kSepRMax + 1];
@@ -686,8 +795,15 @@ __global__ __launch_bounds__(256) void fog_sep_v(const float4* __restrict__ tmp,
   double sa, sb;
   sep_sizes(MODE, band, fp, ka, sa, kb, sb);
   if (MODE == kSepBand && ka <= 1) return;
-  gauss_half(ka, sa, kA);
-  gauss_half(kb, sb, kB);
+  {
+    const float* tb = tab + (size_t)b * kTabStride;
+    const int oa = MODE == kSepGlow ? kTabGlowA : kTabBand + 32 * band;
+    const int ob = MODE == kSepGlow ? kTabGlowB : kTabBand + 32 * band;
+    if (threadIdx.x <= kSepRMax) {
+      kA[threadIdx.x] = tb[oa + threadIdx.x];
+      kB[threadIdx.x] = tb[ob + threadIdx.x];
+    }
+  }
   const int ra = ka / 2, rb = kb / 2, R = max(ra, rb);
   const float4* s = tmp + (size_t)b * H * W;
   for (int i = threadIdx.x; i < (kVRows + 2 * R) * kVCols; i += blockDim.x) {
@@ -738,8 +854,8 @@ __global__ __launch_bounds__(256) void fog_sep_v(const float4* __restrict__ tmp,
 constexpr int kFW = 64, kFH = 16;
 __global__ __launch_bounds__(256) void fog_fade_kernel(
     const float4* __restrict__ h1, int H, int W, const float* __restrict__ fparams,
-    const float* __restrict__ noise, FogConsts c, uint8_t* __restrict__ out, int pitch,
-    size_t fstride) {
+    const float* __restrict__ noise, const float* __restrict__ tab, FogConsts c,
+    uint8_t* __restrict__ out, int pitch, size_t fstride) {
   __shared__ int ytile[(kFH + 2 * kFadeRMax) * (kFW + 2 * kFadeRMax)];
   __shared__ float cw[256];
   __shared__ float sw[kFadeRMax * kFadeRMax + 1];
@@ -747,10 +863,9 @@ __global__ __launch_bounds__(256) void fog_fade_kernel(
   const float* fp = fparams + (size_t)b * RV_FOG_NPARAM_FULL;
   const float amount = fp[11];
   const int rad = min(max((int)fp[18] / 2, 1), kFadeRMax);
-  const double sig = 25.0 + (double)amount * 50.0;
-  const double coef = -0.5 / (sig * sig);
-  cw[threadIdx.x] = (float)exp((double)threadIdx.x * threadIdx.x * coef);
-  if ((int)threadIdx.x <= rad * rad) sw[threadIdx.x] = (float)exp((double)threadIdx.x * coef);
+  const float* tb = tab + (size_t)b * kTabStride;
+  cw[threadIdx.x] = tb[kTabCw + threadIdx.x];
+  if ((int)threadIdx.x <= rad * rad) sw[threadIdx.x] = tb[kTabSw + threadIdx.x];
   const int TW = kFW + 2 * rad, TH = kFH + 2 * rad;
   const float4* src = h1 + (size_t)b * H * W;
   for (int i = threadIdx.x; i < TW * TH; i += blockDim.x) {
@@ -810,9 +925,14 @@ __global__ __launch_bounds__(256) void fog_fade_kernel(
   }
 }
 
+// _airlight_from_image's band rows, max(10, int(0.12 h)) (fog.py:122).
+inline int air_band_rows(int H) { return max(10, (int)(0.12 * H)); }
+
 // Workspace layout of rv_fog_full_u8.
 struct FullWs {
-  float *range, *part, *air, *ascale, *gthr;
+  float *range, *part, *air, *ascale, *gthr, *tab;
+  uint32_t *keys, *hist;
+  AirState* st;
   double *apart, *gpart;
   float *t0, *tf;
   float4 *h1, *tmp, *h2;
@@ -834,6 +954,10 @@ FullWs full_ws(void* base, int B, int H, int W) {
   w.air = (float*)take((size_t)B * 4 * sizeof(float));
   w.ascale = (float*)take((size_t)B * sizeof(float));
   w.gthr = (float*)take((size_t)B * sizeof(float));
+  w.tab = (float*)take((size_t)B * kTabStride * sizeof(float));
+  w.hist = (uint32_t*)take((size_t)B * 2048 * sizeof(uint32_t));
+  w.st = (AirState*)take((size_t)B * sizeof(AirState));
+  w.keys = (uint32_t*)take((size_t)B * air_band_rows(H) * W * sizeof(uint32_t));
   w.apart = (double*)take((size_t)B * kFullNblk * sizeof(double));
   w.gpart = (double*)take((size_t)B * kFullNblk * 2 * sizeof(double));
   w.t0 = (float*)take(px * sizeof(float));
@@ -964,7 +1088,7 @@ extern "C" int rv_fog_full_u8(const uint8_t* in, uint8_t* out, int B, int H, int
   f.q_t = full[2];
   f.edge_guided = full[3] != 0.f;
   f.nblk = min(kFullNblk, ceil_div(H * W, 256));
-  RV_CHECK_ARG(f.band_h >= 1 && f.band_h <= H && f.q_k >= 0 && f.q_k < f.band_h * W &&
+  RV_CHECK_ARG(f.band_h >= 1 && f.band_h <= H && f.band_h <= air_band_rows(H) && f.q_k >= 0 && f.q_k < f.band_h * W &&
                    f.q_t >= 0.f && f.q_t < 1.f,
                "bad airlight band constants");
   if (B == 0) return RV_OK;
@@ -977,14 +1101,32 @@ extern "C" int rv_fog_full_u8(const uint8_t* in, uint8_t* out, int B, int H, int
   const int rblocks = min(kRangeBlocks, ceil_div(H * W, 256));
   fog_range_kernel<<<dim3(rblocks, B), 256, 0, s>>>(grids, taps, c, H, W, w.part);
   fog_range_finish<<<B, 256, 0, s>>>(w.part, rblocks, w.range);
-  fog_air_kernel<<<B, kAirThreads, 0, s>>>(in, W, pitch, fstride, f, frame_params, w.air);
+  fog_taps_kernel<<<B, 256, 0, s>>>(frame_params, w.tab);
+  {  // image airlight: band quantile + masked mean (fog.py:120-130)
+    const int n = f.band_h * W;
+    const dim3 ga(ceil_div(n, kAirPerBlock), B);
+    int rc = hip_check(hipMemsetAsync(w.hist, 0, (size_t)B * 2048 * sizeof(uint32_t), s),
+                       "hipMemsetAsync(hist)");
+    if (rc == RV_OK)
+      rc = hip_check(hipMemsetAsync(w.st, 0, (size_t)B * sizeof(AirState), s),
+                     "hipMemsetAsync(air state)");
+    if (rc != RV_OK) return rc;
+    fog_lum_kernel<<<ga, 256, 0, s>>>(in, W, pitch, fstride, n, w.keys, w.hist);
+    fog_sel_kernel<<<B, 256, 0, s>>>(w.hist, 21, 2048, 1, f.q_k, w.st);
+    fog_hist_kernel<<<ga, 256, 0, s>>>(w.keys, n, 10, 2048, w.st, w.hist);
+    fog_sel_kernel<<<B, 256, 0, s>>>(w.hist, 10, 2048, 0, f.q_k, w.st);
+    fog_hist_kernel<<<ga, 256, 0, s>>>(w.keys, n, 0, 1024, w.st, w.hist);
+    fog_sel_kernel<<<B, 256, 0, s>>>(w.hist, 0, 1024, 0, f.q_k, w.st);
+    fog_airsum_kernel<<<ga, 256, 0, s>>>(in, W, pitch, fstride, n, w.keys, w.st);
+    fog_airfin_kernel<<<B, 1, 0, s>>>(w.st, f, n, frame_params, w.air);
+  }
   fog_t_kernel<<<dim3(f.nblk, B), 256, 0, s>>>(grids, taps, c, f, H, W, depth, amap_unit,
                                                frame_params, w.range, w.air, w.t0, w.apart);
   fog_sum_finish<<<B, 256, 0, s>>>(w.apart, f.nblk, 1, 3.0 * H * W, frame_params, 0, w.ascale);
   const float* tf = w.t0;
   if (f.edge_guided) {
     fog_tbil_kernel<<<dim3(ceil_div(W, kTbW), ceil_div(H, kTbH), B), 256, 0, s>>>(w.t0, H, W,
-                                                                                w.tf);
+                                                                                w.tab, w.tf);
     tf = w.tf;
   }
   fog_scatter_kernel<<<dim3(f.nblk, B), 256, 0, s>>>(in, H, W, pitch, fstride, scene, amap_unit,
@@ -992,14 +1134,17 @@ extern "C" int rv_fog_full_u8(const uint8_t* in, uint8_t* out, int B, int H, int
   fog_sum_finish<<<B, 256, 0, s>>>(w.gpart, f.nblk, 2, (double)H * W, frame_params, 1, w.gthr);
   const dim3 gh(ceil_div(W, 256), H, B), gv(ceil_div(W, kVCols), ceil_div(H, kVRows), B);
   const size_t vlds = (size_t)(kVRows + 2 * kSepRMax) * kVCols * sizeof(float4);
-  fog_sep_h<kSepGlow><<<gh, 256, 0, s>>>(w.h1, H, W, frame_params, w.gthr, bands, 0, w.tmp);
-  fog_sep_v<kSepGlow><<<gv, 256, vlds, s>>>(w.tmp, H, W, frame_params, 0, w.h1, w.h2);
+  fog_sep_h<kSepGlow><<<gh, 256, 0, s>>>(w.h1, H, W, frame_params, w.tab, w.gthr, bands, 0,
+                                         w.tmp);
+  fog_sep_v<kSepGlow><<<gv, 256, vlds, s>>>(w.tmp, H, W, frame_params, w.tab, 0, w.h1, w.h2);
   for (int band = 0; band < 3; ++band) {
-    fog_sep_h<kSepBand><<<gh, 256, 0, s>>>(w.h2, H, W, frame_params, w.gthr, bands, band, w.tmp);
-    fog_sep_v<kSepBand><<<gv, 256, vlds, s>>>(w.tmp, H, W, frame_params, band, w.h1, w.h2);
+    fog_sep_h<kSepBand><<<gh, 256, 0, s>>>(w.h2, H, W, frame_params, w.tab, w.gthr, bands, band,
+                                           w.tmp);
+    fog_sep_v<kSepBand><<<gv, 256, vlds, s>>>(w.tmp, H, W, frame_params, w.tab, band, w.h1,
+                                              w.h2);
   }
   fog_fade_kernel<<<dim3(ceil_div(W, kFW), ceil_div(H, kFH), B), 256, 0, s>>>(
-      w.h1, H, W, frame_params, noise, c, out, pitch, fstride);
+      w.h1, H, W, frame_params, noise, w.tab, c, out, pitch, fstride);
   return launch_status("rv_fog_full_u8");
 }
 
