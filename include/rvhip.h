@@ -34,6 +34,7 @@ extern "C" {
 #define RV_OK 0
 #define RV_EINVAL (-1000)
 #define RV_ECAP (-1001)
+#define RV_EOF 1 /* rv_capture_*: the source has no more frames */
 
 /* ABI version (bumped on any signature change) and last-error text. */
 int rv_abi_version(void);
@@ -453,6 +454,35 @@ int rv_fog_full_u8(const uint8_t* in, uint8_t* out, int B, int H, int W, int pit
                    const uint8_t* bands, const float* frame_params, const float* grids,
                    int grid_stride, const float* noise, void* ws, size_t ws_bytes,
                    void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Capture front end (VideoSource, src/io_video/capture.py:10-24; README    */
+/* module 8's async pipeline).  One reader thread per source fills a ring of */
+/* pinned host slots from a file; frames are stamped with the wall-clock    */
+/* time they were read (capture.py:20).  Formats: YUV4MPEG2 4:2:0 (handed   */
+/* out as NV12), raw NV12, raw BGR.  No bitstream decoder / camera here.    */
+/* ------------------------------------------------------------------------ */
+#define RV_CAP_Y4M 0
+#define RV_CAP_NV12 1
+#define RV_CAP_BGR 2
+/* W, H are read from the header for Y4M; nbuf in [2, 64] slots; loop != 0
+ * rewinds at end of file.  *handle owns a reader thread. */
+int rv_capture_open(const char* path, int fmt, int W, int H, int nbuf, int loop, void** handle);
+/* info[6] = {W, H, fmt, frame bytes (NV12: 3WH/2, BGR: 3WH), pinned, nbuf} */
+int rv_capture_info(void* handle, int* info);
+/* Next frame in order (blocks until read): RV_OK with the slot's host pointer,
+ * read time (s since the epoch) and frame index, or RV_EOF.  The slot stays
+ * held until rv_capture_release. */
+int rv_capture_next(void* handle, uint8_t** frame, double* ts, int64_t* index, int* slot);
+int rv_capture_release(void* handle, int slot);
+/* One frame of each of S sources -> dev + s * dev_stride (H2D on `stream`);
+ * each slot returns to its reader by a host callback queued behind its copy,
+ * so the rings refill while the device works.  ts / index (host, S) may be
+ * NULL.  RV_EOF when a source ended (frames already queued are still
+ * copied).  Synchronise `stream` before rv_capture_close. */
+int rv_capture_upload_batch(void* const* handles, int S, uint8_t* dev, size_t dev_stride,
+                            double* ts, int64_t* index, void* stream);
+int rv_capture_close(void* handle);
 
 #ifdef __cplusplus
 }

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import c_double, c_float, c_int, c_size_t, c_void_p, POINTER
+from ctypes import c_char_p, c_double, c_float, c_int, c_size_t, c_void_p, POINTER
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "librvhip.so")
@@ -68,6 +68,14 @@ _SIGS = {
     "rv_fog_rain_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_size_t,
                                c_void_p]),
+    # capture front end
+    "rv_capture_open": (c_int, [c_char_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "rv_capture_info": (c_int, [c_void_p, c_void_p]),
+    "rv_capture_next": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rv_capture_release": (c_int, [c_void_p, c_int]),
+    "rv_capture_upload_batch": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p,
+                                        c_void_p]),
+    "rv_capture_close": (c_int, [c_void_p]),
     "rv_fog_full_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
     "rv_fog_full_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
