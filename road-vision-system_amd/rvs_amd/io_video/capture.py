@@ -55,7 +55,7 @@ def write_y4m(path: str, frames_bgr: Sequence[np.ndarray], fps: int = 30) -> Non
     with open(path, "wb") as f:
         f.write(f"YUV4MPEG2 W{W} H{H} F{fps}:1 Ip A1:1 C420jpeg\n".encode())
         for img in frames_bgr:
-            x = img.astype(np.float64)
+            x = img.astype(np.float32)
             b, g, r = x[..., 0], x[..., 1], x[..., 2]
             y = 16 + 0.257 * r + 0.504 * g + 0.098 * b
             u = 128 - 0.148 * r - 0.291 * g + 0.439 * b
