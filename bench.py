@@ -80,6 +80,10 @@ def parse_args(argv=None):
                          "2 = [T(k-1) || P(k)] -> Y(k)")
     ap.add_argument("--graph-chunk", type=int, default=None,
                     help="pipeline steps per captured graph (default 8, RV_GRAPH_CHUNK; 0 = all)")
+    ap.add_argument("--pair", type=int, default=int(os.environ.get("RV_PAIR", 4)),
+                    help="depth 4: run the forwards of this many consecutive steps as one batch "
+                         "(pair x streams frames; SORT still sees every stream in order); the "
+                         "largest divisor of --steps not above it is used")
     ap.add_argument("--lanes", type=int, default=int(os.environ.get("RV_LANES", 1)),
                     help="forward lanes: the YOLO forwards of this many consecutive steps run "
                          "concurrently (engine.OverlappedSteps dependency-graph schedule)")
@@ -100,8 +104,11 @@ class BenchJob:
         self.S, self.K, self.Wm = args.streams, args.steps, args.warmup
         # depth 4 runs the two halves of consecutive forwards on two lanes
         lanes = 2 if args.depth == 4 and not args.no_pipeline and not args.eager else args.lanes
+        pair = 1
+        if args.depth == 4 and not args.no_pipeline and not args.eager:
+            pair = max(p for p in range(1, max(1, args.pair) + 1) if args.steps % p == 0)
         self.eng = RoadVisionEngine(self.cfg, self.S, (H, W), device=dev, tmax=args.tmax,
-                                    lanes=lanes)
+                                    lanes=lanes, pair=pair)
         self.frames = road_frames(self.S, self.Wm + self.K, H, W, device=dev,
                                   stream_offset=rank_streams(self.S, rank).start)
         self.ts = torch.tensor([[f / 30.0] * self.S for f in range(self.Wm + self.K)],
@@ -208,6 +215,13 @@ def _conv_pass(job, mode: str, tags):
         prof = OverlappedSteps(eng, [job.frames[Wm + k] for k in range(K)],
                                [job.ts[Wm + k] for k in range(K)], depth=job.args.depth,
                                chunk=job.args.graph_chunk, capture=False)
+    elif eng.pair > 1:  # each launch alone, on the timed region's forward batch
+        from rvs_amd.handback import Record
+        P = eng.pair
+        recs = [Record(eng.S, eng.detector.max_det, eng.device) for _ in range(P)]
+        for u in range(K // P):
+            eng.step_unit([job.frames[Wm + u * P + h] for h in range(P)],
+                          [job.ts[Wm + u * P + h] for h in range(P)], recs)
     else:
         for k in range(K):
             eng.step(job.frames[Wm + k], job.ts[Wm + k])
@@ -222,8 +236,10 @@ def _conv_pass(job, mode: str, tags):
     torch.cuda.synchronize()
     lib.rv_yolo_profile(h, 0)
     valid = cv >= 0
-    return (float(ms[valid].sum()) / max(nf, 1), float(fl[valid].sum()), float(by[valid].sum()),
-            int(valid.sum()))
+    # pair mode: every profiled forward covers `pair` steps -> per step
+    per = eng.pair
+    return (float(ms[valid].sum()) / max(nf, 1) / per, float(fl[valid].sum()) / per,
+            float(by[valid].sum()) / per, int(valid.sum()) / per)
 
 
 def conv_roofline(job, mode: str) -> dict:
@@ -275,7 +291,8 @@ def conv_roofline(job, mode: str) -> dict:
     main = "eager" if "eager" in res else "overlap"
     out = {"kernel": "conv family: conv_patch_kernel + conv1x1_direct_kernel + c2f_chain_kernel "
                      "(all YOLOv8n conv launches of a step; HIP events on the launch stream)",
-           "timing": main + (" (one step at a time: each launch alone)" if main == "eager" else
+           "timing": main + (" (one pipeline unit at a time: each launch alone, on the timed "
+                             "region's forward batch)" if main == "eager" else
                              " (the timed region's schedule run eagerly)")}
     out.update(view(*res[main]))
     out["traffic"] = traffic
@@ -374,8 +391,12 @@ def main(argv=None):
     sort_rep = job.track_report()
     roof = conv_roofline(job, args.conv_timing) if args.conv_timing != "none" else None
 
-    chunk_desc = (args.graph_chunk if args.graph_chunk is not None
-                  else int(os.environ.get("RV_GRAPH_CHUNK", "8")))
+    P = job.eng.pair
+    if args.graph_chunk is not None:
+        chunk_desc = args.graph_chunk
+    else:
+        chunk_desc = int(os.environ.get("RV_GRAPH_CHUNK", "8"))
+        chunk_desc = max(1, chunk_desc // P) if chunk_desc > 0 and P > 1 else chunk_desc
     chunk_desc = "all" if chunk_desc <= 0 else str(chunk_desc)
     res = {
         "metric": METRIC,
@@ -397,14 +418,17 @@ def main(argv=None):
                    "streams_per_gpu": S, "frame": [H, W],
                    "detector_input": [job.eng.detector.in_h, job.eng.detector.in_w],
                    "parallelism": f"streams sharded {S}/GPU, no collective",
+                   "forward_batch": S * job.eng.pair,
                    "conv_autotune": ("loaded" if args.tune_load else
                                      (not args.no_autotune)),
                    "execution": "eager" if args.eager else
                                 ("graph per step" if args.no_pipeline else
                                  ("graphs, 4-stage software pipeline: stage k runs the second "
-                                  "half of step k-1's forward || preprocess of step k+1 || the "
-                                  "first half of step k's forward || NMS+SORT+hand-back of step "
-                                  f"k-2 (two forward workspaces), {chunk_desc} steps per graph"
+                                  "half of unit k-1's forward || preprocess of unit k+1 || the "
+                                  "first half of unit k's forward || NMS+SORT+hand-back of unit "
+                                  f"k-2 (two forward workspaces; a unit = {job.eng.pair} step(s), "
+                                  f"one forward over their {S * job.eng.pair} frames), "
+                                  f"{chunk_desc} units per graph"
                                   if args.depth == 4 else
                                   f"graphs, dependency-graph pipeline with {args.lanes} concurrent "
                                   "YOLO forwards (preprocess runs ahead, NMS+SORT+hand-back "

@@ -212,9 +212,10 @@ class YoloEngine:
         for h in self._hs:
             call("rv_yolo_set_option", h, 2, 1 if on else 0)
 
-    def letterbox(self, frames: torch.Tensor, slot: int = 0) -> torch.Tensor:
+    def letterbox(self, frames: torch.Tensor, slot: int = 0, off: int = 0) -> torch.Tensor:
+        """Letterbox into images [off, off + B) of letterbox slot `slot`."""
         B = frames.shape[0]
-        return kernels.letterbox(frames, self.geo, out=self.lb[slot][:B])
+        return kernels.letterbox(frames, self.geo, out=self.lb[slot][off:off + B])
 
     def forward_raw(self, lb: Optional[torch.Tensor], raw: Optional[torch.Tensor] = None,
                     candidates: bool = True, slot: int = 0, lane: int = 0, part: int = 0,

@@ -31,10 +31,18 @@ from .track.sort_hip import MultiStreamSort
 class RoadVisionEngine:
     def __init__(self, cfg: Optional[dict], n_streams: int, frame_hw, device="cuda",
                  tmax: int = 1024, projector: Optional[GroundProjector] = None,
-                 weights: Optional[np.ndarray] = None, lanes: int = 1):
+                 weights: Optional[np.ndarray] = None, lanes: int = 1, pair: int = 1):
+        """pair = P >= 2: the pipelined schedule (OverlappedSteps depth 4)
+        runs the forwards of P consecutive steps as one batch of P*S frames
+        (the small P4 / P5 layers amortise their per-launch floor; measured
+        B = 64: 20.5 us per frame against 25.0 at B = 32,
+        tools/probe_batch.py).  Every stream still sees its frames in order
+        in SORT, so results are those of sequential step() calls; a frame's
+        results come out P - 1 steps later."""
         cfg = cfg if cfg is not None else load_config()
         self.cfg = cfg
         self.S = int(n_streams)
+        self.pair = max(1, int(pair))
         self.H, self.W = int(frame_hw[0]), int(frame_hw[1])
         self.device = torch.device(device)
         self.pipeline = PreprocessPipeline(cfg.get("preprocess", {}) or {})
@@ -43,7 +51,8 @@ class RoadVisionEngine:
         if weights is None:
             weights = weights_from_config(det_cfg, self.variant)
         self.detector = YoloEngine(
-            self.variant, weights, self.S, (self.H, self.W), imgsz=int(det_cfg.get("imgsz", 640)),
+            self.variant, weights, self.S * self.pair, (self.H, self.W),
+            imgsz=int(det_cfg.get("imgsz", 640)),
             conf=float(det_cfg.get("conf_thres", 0.25)), iou=float(det_cfg.get("iou_thres", 0.7)),
             max_det=int(det_cfg.get("max_det", 100)),
             classes_keep=[int(x) for x in det_cfg.get("classes_keep", [])], device=self.device,
@@ -65,22 +74,24 @@ class RoadVisionEngine:
         # default chain: CLAHE + median + the detector's LetterBox in one pass
         self.fused_letterbox = self.pipeline.letterbox_fusable(self.H, self.W, self.detector.geo)
 
-    def preprocess_stage(self, frames: torch.Tensor, lb_slot: int = 0):
+    def preprocess_stage(self, frames: torch.Tensor, lb_slot: int = 0, lb_off: int = 0):
         """pipeline(raw) + the detector's LetterBox (main_preview.py:94-99)
         for (S,H,W,3) u8 device frames -> (proc, letterboxed batch in the
-        detector's letterbox slot `lb_slot`)."""
+        detector's letterbox slot `lb_slot`, images [lb_off, lb_off + S))."""
+        B = frames.shape[0]
         if self.fused_letterbox:
             return self.pipeline.run_with_letterbox(frames, self.detector.geo,
-                                                    self.detector.lb[lb_slot][:frames.shape[0]])
+                                                    self.detector.lb[lb_slot][lb_off:lb_off + B])
         proc = self.pipeline(frames)
-        return proc, self.detector.letterbox(proc, lb_slot)
+        return proc, self.detector.letterbox(proc, lb_slot, lb_off)
 
     def yolo_stage(self, lb: Optional[torch.Tensor], slot: int = 0, lane: int = 0,
                    part: int = 0) -> None:
         """YOLOv8 forward + decode in forward context `lane`; NMS candidates
         land in candidate slot `slot`.  part 1 / 2: the two halves of the
         forward (YoloEngine.forward_raw)."""
-        self.detector.forward_raw(lb, slot=slot, lane=lane, part=part, batch=self.S)
+        self.detector.forward_raw(lb, slot=slot, lane=lane, part=part,
+                                  batch=self.S if lb is not None else self.S * self.pair)
 
     def detect_stage(self, frames: torch.Tensor, slot: int = 0) -> torch.Tensor:
         proc, lb = self.preprocess_stage(frames)
@@ -89,8 +100,11 @@ class RoadVisionEngine:
 
     def autotune(self, frames: torch.Tensor, reps: int = 3, verify: bool = False) -> int:
         """Autotune the detector's conv kernels on one batch of these frames
-        (YoloEngine.autotune); call outside graph capture."""
-        _, lb = self.preprocess_stage(frames)
+        (YoloEngine.autotune; pair mode: the batch of P*S the pipelined
+        forwards run, the frames repeated); call outside graph capture."""
+        for h in range(self.pair):
+            self.preprocess_stage(frames, 0, h * self.S)
+        lb = self.detector.lb[0][:self.S * self.pair]
         return self.detector.autotune(lb, reps=reps, verify=verify)
 
     def track_stage(self, ts: torch.Tensor, slot: int = 0,
@@ -105,6 +119,33 @@ class RoadVisionEngine:
             handback(dets, det_n, tid, dist, spd, self.rec_stage, record.host)
             out["record"] = record
         return out
+
+    def track_pair_stage(self, ts_list, slot: int, records) -> List[Dict[str, torch.Tensor]]:
+        """Pair mode: NMS of the P*S images of candidate slot `slot` at once,
+        then SORT + hand-back of each of the P steps in order (step h owns
+        images [h*S, (h+1)*S))."""
+        S = self.S
+        dets, det_n = self.detector.nms(S * len(ts_list), slot)
+        outs = []
+        for h, (ts, rec) in enumerate(zip(ts_list, records)):
+            d, n = dets[h * S:(h + 1) * S], det_n[h * S:(h + 1) * S]
+            tid, dist, spd = self.tracker.update(d, n, ts)
+            handback(d, n, tid, dist, spd, self.rec_stage, rec.host)
+            outs.append({"record": rec})
+        return outs
+
+    def step_unit(self, frames_list, ts_list, records) -> List[Dict[str, torch.Tensor]]:
+        """Pair mode, sequentially on the current stream: the preprocess of
+        P consecutive steps into one letterbox slot, ONE forward over their
+        P*S frames, then NMS + per-step SORT + hand-back (the work of one
+        pipeline unit of OverlappedSteps, each launch alone)."""
+        S = self.S
+        procs = [self.preprocess_stage(f, 0, h * S)[0] for h, f in enumerate(frames_list)]
+        self.yolo_stage(self.detector.lb[0][:S * len(frames_list)], 0)
+        outs = self.track_pair_stage(ts_list, 0, records)
+        for o, p in zip(outs, procs):
+            o["proc"] = p
+        return outs
 
     def step(self, frames: torch.Tensor, ts: torch.Tensor) -> Dict[str, torch.Tensor]:
         """frames (S,H,W,3) u8 on device, ts (S,) f64 on device.  The step's
@@ -201,6 +242,8 @@ class OverlappedSteps:
         run() replays them chained by HIP events (_issue); `chunk` does not
         apply."""
         self.eng = eng
+        if eng.pair > 1 and depth != 4:
+            raise ValueError("RoadVisionEngine(pair > 1) runs the depth-4 pipeline only")
         ctx = (lambda g: torch.cuda.graph(g)) if capture else (lambda g: contextlib.nullcontext())
         K = len(frames)
         dev = eng.device
@@ -215,8 +258,10 @@ class OverlappedSteps:
         def track(j):
             o = eng.track_stage(ts[j], j % slots, self.records[j])
             return {"record": o["record"]}
-        if chunk is None:
+        if chunk is None:  # default: 8 steps per graph (pair mode: 8 // pair units)
             chunk = int(os.environ.get("RV_GRAPH_CHUNK", "8"))
+            if chunk > 0 and eng.pair > 1:
+                chunk = max(1, chunk // eng.pair)
         self.staged = L > 1 and depth != 4
         if self.staged:
             # Per-stage graphs chained by events at replay time (run()): a
@@ -273,7 +318,7 @@ class OverlappedSteps:
             return
         lbs = {}
         if depth == 4:
-            self._capture_depth4(frames, track, procs, lbs, chunk, ctx, capture)
+            self._capture_depth4(frames, ts, track, procs, lbs, chunk, ctx, capture)
             return
         # steps per captured graph (`chunk`, RV_GRAPH_CHUNK): consecutive
         # pipeline stages j are captured into one graph, so the device never
@@ -305,7 +350,7 @@ class OverlappedSteps:
             if capture:
                 self.graphs.append(g)
 
-    def _capture_depth4(self, frames, track, procs, lbs, chunk, ctx, capture):
+    def _capture_depth4(self, frames, ts, track, procs, lbs, chunk, ctx, capture):
         """depth=4 with two forward lanes: the forward is split in two
         (rv_yolo_forward_part) and stage j runs
             P(j+1) || Y1(j) || Y2(j-1) || T(j-2)
@@ -315,12 +360,25 @@ class OverlappedSteps:
         NMS + SORT of step j-2.  Y2 runs on the capture stream (it forks the
         Detect heads); Y1, P and T on side streams."""
         eng = self.eng
-        K = len(frames)
         if eng.detector.lanes != 2:
             raise ValueError("depth 4 needs RoadVisionEngine(lanes=2)")
+        P = eng.pair
+        if len(frames) % P:
+            raise ValueError(f"pair mode: the step count {len(frames)} is not a multiple of {P}")
+        K = len(frames) // P  # pipeline units: P consecutive steps, one forward
         dev = eng.device
         side_p, side_t, side_y = (torch.cuda.Stream(dev) for _ in range(3))
         slots = eng.detector.slots
+        S = eng.S
+        if P > 1:  # a unit's stages over its P steps
+            def prep(u, slot):
+                for h in range(P):
+                    procs[u * P + h], _ = eng.preprocess_stage(frames[u * P + h], slot, h * S)
+                return None, eng.detector.lb[slot][:P * S]
+
+            def trk(u, slot):
+                return eng.track_pair_stage([ts[u * P + h] for h in range(P)], slot,
+                                            [self.records[u * P + h] for h in range(P)])
         js = list(range(-1, K + 2))
         size = len(js) if chunk <= 0 else chunk
         for c0 in range(0, len(js), size):
@@ -335,13 +393,17 @@ class OverlappedSteps:
                     def p_(j=j):  # P(j+1) into letterbox slot (j+1) % slots
                         if 0 <= j + 1 < K:
                             with torch.cuda.stream(side_p):
-                                procs[j + 1], lbs[j + 1] = eng.preprocess_stage(
-                                    frames[j + 1], (j + 1) % slots)
+                                if P > 1:
+                                    _, lbs[j + 1] = prep(j + 1, (j + 1) % slots)
+                                else:
+                                    procs[j + 1], lbs[j + 1] = eng.preprocess_stage(
+                                        frames[j + 1], (j + 1) % slots)
 
                     def t_(j=j):  # T(j-2) from candidate slot (j-2) % slots
                         if 0 <= j - 2 < K:
                             with torch.cuda.stream(side_t):
-                                res["out"] = track(j - 2)
+                                res["out"] = (trk(j - 2, (j - 2) % slots) if P > 1
+                                              else track(j - 2))
 
                     def y1_(j=j):  # Y1(j) on lane j % 2
                         if 0 <= j < K:
@@ -363,8 +425,9 @@ class OverlappedSteps:
                     for x in (side_p, side_t, side_y):
                         cur.wait_stream(x)
                     if 0 <= j - 2 < K:
-                        out["proc"] = procs.pop(j - 2)
-                        self.outs.append(out)
+                        for h, o in enumerate(out if P > 1 else [out]):
+                            o["proc"] = procs.pop((j - 2) * P + h)
+                            self.outs.append(o)
             if capture:
                 self.graphs.append(g)
 

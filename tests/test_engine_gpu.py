@@ -110,21 +110,24 @@ def test_results_record_matches_device_outputs(cuda):
     eng.close()
 
 
-@pytest.mark.parametrize("depth,chunk,lanes", [(2, None, 1), (3, 1, 1), (3, 3, 1), (3, None, 1),
-                                               (3, 0, 1), (3, None, 2), (3, 3, 2), (3, 0, 3),
-                                               (4, None, 2), (4, 3, 2), (4, 0, 2)])
-def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk, lanes):
+@pytest.mark.parametrize("depth,chunk,lanes,pair", [
+    (2, None, 1, 1), (3, 1, 1, 1), (3, 3, 1, 1), (3, None, 1, 1), (3, 0, 1, 1), (3, None, 2, 1),
+    (3, 3, 2, 1), (3, 0, 3, 1), (4, None, 2, 1), (4, 3, 2, 1), (4, 0, 2, 1), (4, None, 2, 2),
+    (4, 1, 2, 2)])
+def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk, lanes, pair):
     """bench.py's timed mode (engine.OverlappedSteps): the track stage of step
     k runs on a side stream beside the preprocess of step k+1, with `chunk`
     pipeline stages per captured graph (None = the default 8, 0 = one graph);
     lanes >= 2 (depth 3): the dependency-graph schedule with that many concurrent YOLO
-    forwards.  EVERY step's handed-back detections / track ids and proc
+    forwards; pair 2 (depth 4): one forward over two consecutive steps'
+    frames.  EVERY step's handed-back detections / track ids and proc
     frames, and the final SORT state, must equal those of plain sequential
     step() calls."""
     from rvs_amd.engine import OverlappedSteps, RoadVisionEngine
     from rvs_amd.synth import road_frames
     cfg = _cfg()
-    S, H, W, F = 4, 1080, 1920, 8
+    S, H, W = 4, 1080, 1920
+    F = 9 if pair == 2 else 8  # the overlapped steps (F - 1) pair up
     frames = road_frames(S, F, H, W, device=cuda)
     ts = torch.tensor([[f / 30.0] * S for f in range(F)], dtype=torch.float64, device=cuda)
     seq = RoadVisionEngine(cfg, S, (H, W), device=cuda)
@@ -133,7 +136,7 @@ def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk, lanes):
         out_seq = seq.step(frames[f], ts[f])
         seq_res.append(seq.results(out_seq))
         seq_proc.append(out_seq["proc"].cpu().numpy())
-    ovl = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=lanes)
+    ovl = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=lanes, pair=pair)
     ovl.step(frames[0], ts[0])  # eager first step (one-time kernel setup)
     run = OverlappedSteps(ovl, [frames[f] for f in range(1, F)], [ts[f] for f in range(1, F)],
                           depth=depth, chunk=chunk)
@@ -155,11 +158,12 @@ def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk, lanes):
     ovl.close()
 
 
-@pytest.mark.parametrize("depth,lanes", [(4, 2), (3, 1)])
-def test_bench_configuration_parity(cuda, depth, lanes):
+@pytest.mark.parametrize("depth,lanes,pair", [(4, 2, 1), (4, 2, 4), (3, 1, 1)])
+def test_bench_configuration_parity(cuda, depth, lanes, pair):
     """Exactly bench.py's timed configuration (S = 32 streams of 1080p,
     autotuned conv kernels, OverlappedSteps(depth=4, chunk=8) on two forward
-    lanes -- and the depth-3 one-lane pipeline --, hand-back into per-step
+    lanes, with and without pairing two steps per forward -- and the depth-3
+    one-lane pipeline --, hand-back into per-step
     host records), checked against the oracle on every step:
     proc bit-exact on a sample of streams, NMS exact on the GPU's raw
     prediction for all 32 streams, SORT ids / distances exact for all 32
@@ -168,7 +172,7 @@ def test_bench_configuration_parity(cuda, depth, lanes):
     from rvs_amd.synth import road_frames
     cfg = _cfg()
     S, H, W, WARM, K = 32, 1080, 1920, 2, 8
-    eng = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=lanes)
+    eng = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=lanes, pair=pair)
     frames = road_frames(S, WARM + K, H, W, device=cuda)
     ts = torch.tensor([[f / 30.0] * S for f in range(WARM + K)], dtype=torch.float64, device=cuda)
     chk = Checker(eng, cfg, proc_streams=[0, 13, 31])
