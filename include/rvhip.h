@@ -479,7 +479,7 @@ int rv_capture_release(void* handle, int slot);
  * each slot returns to its reader by a host callback queued behind its copy,
  * so the rings refill while the device works.  ts / index (host, S) may be
  * NULL.  RV_EOF when a source ended (frames already queued are still
- * copied).  Synchronise `stream` before rv_capture_close. */
+ * copied).  rv_capture_close waits for queued slot releases. */
 int rv_capture_upload_batch(void* const* handles, int S, uint8_t* dev, size_t dev_stride,
                             double* ts, int64_t* index, void* stream);
 int rv_capture_close(void* handle);

@@ -17,6 +17,7 @@
 // Formats: YUV4MPEG2 (.y4m, 4:2:0 planar, converted to NV12 by the reader
 // thread: U/V interleave), raw NV12, raw BGR.  There is no bitstream decoder
 // in this image (no rocDecode), and no V4L2 camera: DESIGN.md §(f)4.
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -55,6 +56,10 @@ struct Capture {
   bool stop = false, eof = false;
   int err = RV_OK;
   int64_t count = 0;
+  // slot-release callbacks queued in streams and not yet finished: close
+  // waits for them (a stream can read as complete before its host function
+  // has returned), so no callback ever touches a freed Capture
+  std::atomic<int> pending{0};
 };
 
 double wall_now() {
@@ -177,8 +182,10 @@ struct Release {
 
 void release_cb(void* p) {
   Release* r = static_cast<Release*>(p);
-  give_back(r->c, r->slot);
+  Capture* c = r->c;
+  give_back(c, r->slot);
   delete r;
+  c->pending.fetch_sub(1);  // the last access to c
 }
 
 }  // namespace
@@ -294,9 +301,12 @@ extern "C" int rv_capture_upload_batch(void* const* handles, int S, uint8_t* dev
     int e = hip_check(hipMemcpyAsync(dev + (size_t)s * dev_stride, c->slots[slot].p,
                                      c->frame_bytes, hipMemcpyHostToDevice, st),
                       "hipMemcpyAsync(capture)");
-    if (e == RV_OK)
+    if (e == RV_OK) {
+      c->pending.fetch_add(1);
       e = hip_check(hipLaunchHostFunc(st, release_cb, new Release{c, slot}),
                     "hipLaunchHostFunc(capture release)");
+      if (e != RV_OK) c->pending.fetch_sub(1);
+    }
     if (e != RV_OK) {
       give_back(c, slot);
       return e;
@@ -308,6 +318,15 @@ extern "C" int rv_capture_upload_batch(void* const* handles, int S, uint8_t* dev
 extern "C" int rv_capture_close(void* handle) {
   if (!handle) return RV_OK;
   Capture* c = static_cast<Capture*>(handle);
+  // queued slot releases first (bounded: 10 s, then the capture is leaked
+  // rather than freed under a callback)
+  for (int i = 0; c->pending.load() > 0; ++i) {
+    if (i == 100000) {
+      set_error("rv_capture_close: %d slot releases still queued", c->pending.load());
+      return RV_EINVAL;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
   {
     std::lock_guard<std::mutex> lk(c->m);
     c->stop = true;
