@@ -46,8 +46,8 @@ def main():
     K = job.K
     orig_p, orig_y, orig_t = eng.preprocess_stage, eng.yolo_stage, eng.track_stage
 
-    def p_letterbox(frames, lb_slot=0):
-        lb = eng.detector.letterbox(frames, lb_slot)
+    def p_letterbox(frames, lb_slot=0, lb_off=0):
+        lb = eng.detector.letterbox(frames, lb_slot, lb_off)
         return frames, lb
 
     def y_skip(skip):
@@ -60,21 +60,27 @@ def main():
         dets, det_n = eng.detector.nms(ts.shape[0], slot)
         return {"dets": dets, "det_n": det_n, "record": record}
 
+    def t_nms_pair(ts_list, slot, records):
+        eng.detector.nms(eng.S * len(ts_list), slot)
+        return [{"record": r} for r in records]
+    orig_tp = eng.track_pair_stage
+
     out = {}
     out["base"] = timed(job, K)
     eng.preprocess_stage = p_letterbox
     out["P_letterbox_only"] = timed(job, K)
     eng.preprocess_stage = orig_p
-    eng.track_stage = t_nms
+    eng.track_stage, eng.track_pair_stage = t_nms, t_nms_pair
     out["T_nms_only"] = timed(job, K)
-    eng.track_stage = orig_t
+    eng.track_stage, eng.track_pair_stage = orig_t, orig_tp
     eng.yolo_stage = y_skip(2)
     out["no_Y2"] = timed(job, K)
     eng.yolo_stage = y_skip(1)
     out["no_Y1"] = timed(job, K)
     eng.yolo_stage = orig_y
     out["base_again"] = timed(job, K)
-    print(json.dumps({k: round(v, 4) for k, v in out.items()} | {"unit": "ms per 32-frame step"}))
+    print(json.dumps({k: round(v, 4) for k, v in out.items()} |
+                     {"unit": "ms per 32-frame step", "pair": eng.pair}))
 
 
 if __name__ == "__main__":
