@@ -92,6 +92,12 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def pick_pair(steps: int, pair: int) -> int:
+    """Steps per pipeline unit: the largest p <= pair that divides `steps`
+    (a driver may pass any --steps)."""
+    return max(p for p in range(1, max(1, pair) + 1) if steps % p == 0)
+
+
 class BenchJob:
     """What one rank runs: its 32 camera streams through the full chain."""
 
@@ -106,7 +112,7 @@ class BenchJob:
         lanes = 2 if args.depth == 4 and not args.no_pipeline and not args.eager else args.lanes
         pair = 1
         if args.depth == 4 and not args.no_pipeline and not args.eager:
-            pair = max(p for p in range(1, max(1, args.pair) + 1) if args.steps % p == 0)
+            pair = pick_pair(args.steps, args.pair)
         self.eng = RoadVisionEngine(self.cfg, self.S, (H, W), device=dev, tmax=args.tmax,
                                     lanes=lanes, pair=pair)
         self.frames = road_frames(self.S, self.Wm + self.K, H, W, device=dev,

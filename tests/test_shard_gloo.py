@@ -135,3 +135,13 @@ def test_partition_rejects_uneven_split():
     assert rank_streams(32, 3) == range(96, 128)
     with pytest.raises(ValueError):
         partition(10, 4)
+
+
+def test_pick_pair_divides_the_step_count():
+    """bench.py's pipeline unit: the largest pair <= --pair dividing --steps,
+    so any driver step count runs (pair mode needs whole units)."""
+    import bench
+    assert bench.pick_pair(60, 4) == 4 and bench.pick_pair(20, 4) == 4
+    assert bench.pick_pair(10, 4) == 2 and bench.pick_pair(9, 4) == 3
+    assert bench.pick_pair(7, 4) == 1 and bench.pick_pair(5, 1) == 1 and bench.pick_pair(3, 0) == 1
+    assert bench.parse_args([]).pair == 4
