@@ -89,7 +89,16 @@ class PreprocessPipeline:
                 if not bool(low[0]):
                     return image  # contrast is sufficient -> skip the chain
                 return _back(self._run_chain(x), was_np)
-            out = self._run_chain(x)
-            keep = (~low).view(-1, 1, 1, 1)
-            return _back(torch.where(keep, x, out), was_np)
+            # per frame, as the reference's per-frame loop does: only the
+            # low-contrast frames run the chain (gathered into one batch, one
+            # host read of the gate); the others pass through unchanged
+            sel = torch.nonzero(low).flatten()
+            n = int(sel.numel())
+            if n == 0:
+                return image
+            if n == x.shape[0]:
+                return _back(self._run_chain(x), was_np)
+            out = x.clone()
+            out.index_copy_(0, sel, self._run_chain(x.index_select(0, sel).contiguous()))
+            return _back(out, was_np)
         return _back(self._run_chain(x), was_np)

@@ -104,6 +104,31 @@ def test_pipeline_matches_reference_semantics(cuda):
     flat = np.full((32, 32, 3), 90, np.uint8)
     flat[0, 0] = 95
     np.testing.assert_array_equal(p2(flat), cpu.median(cpu.clahe_ycrcb(flat), 5))
+    # batched gate: low-contrast frames run the chain, the others pass through
+    # untouched (the chain is only run on the gathered low-contrast frames)
+    import torch
+    frames = []
+    for i in range(5):
+        f = road_frame(48, 64, seed=40 + i)
+        if i in (1, 3):  # squeeze to a span < 20
+            f = (90 + (f.astype(np.int32) - 90) // 16).clip(0, 255).astype(np.uint8)
+        frames.append(f)
+    batch = np.stack(frames)
+    span = [int(cpu_gray_span(f)) for f in frames]
+    assert [s < 20 for s in span] == [False, True, False, True, False]
+    got = p2(torch.from_numpy(batch).to(cuda)).cpu().numpy()
+    for i, f in enumerate(frames):
+        want = cpu.median(cpu.clahe_ycrcb(f), 5) if span[i] < 20 else f
+        np.testing.assert_array_equal(got[i], want)
+    flat_batch = torch.from_numpy(batch[[0, 2]].copy()).to(cuda)
+    assert p2(flat_batch) is flat_batch  # no low-contrast frame: input returned
+
+
+def cpu_gray_span(img):
+    """cv2.cvtColor BGR2GRAY (14-bit) max - min (pipeline.py:24-30)."""
+    i = img.astype(np.int32)
+    g = (i[..., 0] * 1868 + i[..., 1] * 9617 + i[..., 2] * 4899 + 8192) >> 14
+    return g.max() - g.min()
 
 
 def test_median_vector_path_ragged_width(cuda):
