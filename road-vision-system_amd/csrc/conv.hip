@@ -2067,27 +2067,15 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
     for (int i = 0; i < REG; ++i) e += (float)i * (v[i] * rs);
     d = e;
   }
-  // classes part, part+4, ...: first maximum of the sigmoid scores.  An
-  // anchor whose largest class logit is below logit(conf) - 0.01 cannot be
-  // a candidate (every score <= sigmoid(logit(conf) - 0.01) = conf -
-  // 0.01 conf (1 - conf) + O(1e-4), far below conf even with the ~1 ulp
-  // hardware exp / rcp), so its sigmoids are skipped -- most anchors: the
-  // candidate list is unchanged, bit for bit.
+  // classes part, part+4, ...: first maximum of the sigmoid scores
   const float* pc = px + 4 * REG;
-  float lmax = -INFINITY;
-  for (int c = part; c < nc; c += 4) lmax = fmaxf(lmax, pc[c]);
-  lmax = fmaxf(lmax, __shfl_xor(lmax, 1));
-  lmax = fmaxf(lmax, __shfl_xor(lmax, 2));
-  const bool skip = conf > 0.f && conf < 1.f && lmax < __logf(conf / (1.f - conf)) - 0.01f;
   float best = -1.f;
   int bc = 0;
-  if (!skip) {
-    for (int c = part; c < nc; c += 4) {
-      const float sg = head_sigmoid(pc[c]);
-      if (sg > best) {
-        best = sg;
-        bc = c;
-      }
+  for (int c = part; c < nc; c += 4) {
+    const float sg = head_sigmoid(pc[c]);
+    if (sg > best) {
+      best = sg;
+      bc = c;
     }
   }
   // quad reduction: larger score, then smaller class index
