@@ -1,6 +1,10 @@
-"""Two eager bench steps (autotuned convs) (32 streams x 1080p, full chain) for rocprofv3
---pmc passes: every dispatch of the second step is one row per counter in
-counter_collection.csv (tools/pmc_report.py summarises it)."""
+"""Eager bench work (autotuned convs, 32 streams x 1080p, full chain) for
+rocprofv3 --pmc passes: one warm-up step, then one pipeline unit as the timed
+region runs it (PAIR = 4 steps: four preprocess passes, ONE forward over their
+128 frames, NMS, four SORT + hand-back) -- every dispatch is one row per
+counter in counter_collection.csv (tools/pmc_report.py summarises the window
+from the last LUT pass; tools/pmc_traffic.py divides the unit's conv bytes
+by PAIR)."""
 import os
 import sys
 
@@ -13,12 +17,18 @@ from rvs_amd.engine import RoadVisionEngine  # noqa: E402
 from rvs_amd.synth import road_frames  # noqa: E402
 
 S = int(os.environ.get("S", 32))
+P = int(os.environ.get("PAIR", 4))
 dev = torch.device("cuda:0")
-eng = RoadVisionEngine(bench.bench_config(), S, (1080, 1920), device=dev)
-frames = road_frames(S, 2, 1080, 1920, device=dev)
-ts = torch.tensor([[f / 30.0] * S for f in range(2)], dtype=torch.float64, device=dev)
+eng = RoadVisionEngine(bench.bench_config(), S, (1080, 1920), device=dev, pair=P)
+frames = road_frames(S, 1 + P, 1080, 1920, device=dev)
+ts = torch.tensor([[f / 30.0] * S for f in range(1 + P)], dtype=torch.float64, device=dev)
 eng.step(frames[0], ts[0])
-eng.autotune(frames[0])  # the bench's kernel configurations
-eng.step(frames[1], ts[1])
+eng.autotune(frames[0])  # the bench's kernel configurations (at the unit's batch)
+if P > 1:
+    from rvs_amd.handback import Record
+    recs = [Record(S, eng.detector.max_det, dev) for _ in range(P)]
+    eng.step_unit([frames[1 + h] for h in range(P)], [ts[1 + h] for h in range(P)], recs)
+else:
+    eng.step(frames[1], ts[1])
 torch.cuda.synchronize()
 print("pmc_step done")

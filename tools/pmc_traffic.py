@@ -36,12 +36,17 @@ def main():
         if name.startswith(CONV_KERNELS):
             fetch += rd
             write += wr
+    unit = int(os.environ.get("PAIR", 4))  # steps per profiled forward (tools/pmc_step.py)
+    fetch, write = fetch / unit, write / unit
     res = {"conv_bytes_per_step": fetch + write, "conv_read_bytes": fetch,
            "conv_write_bytes": write, "conv_kernels": list(CONV_KERNELS),
+           "steps_per_forward": unit,
            "per_kernel": {k: {"launches": c, "read_bytes": r, "write_bytes": w}
                           for k, (c, r, w) in per_kernel.items()},
-           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over one eager bench step "
-                     "(tools/gpu_pmc.sh); read = 2 x FETCH_SIZE (gfx950 calibration), KB -> B"}
+           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over one eager pipeline "
+                     "unit (tools/gpu_pmc.sh, tools/pmc_step.py: one forward over PAIR steps' "
+                     "frames, conv bytes / PAIR per step); read = 2 x FETCH_SIZE (gfx950 "
+                     "calibration), KB -> B"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "per_kernel"}))
 
