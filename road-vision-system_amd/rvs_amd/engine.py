@@ -218,6 +218,11 @@ class OverlappedSteps:
     epilogue graph fills and drains the pipeline.  Replayed in order, the K
     steps give the same results as K step() calls (tests/test_engine_gpu.py).
 
+    With an engine of pair = P > 1 (depth 4 only) a pipeline unit is P
+    consecutive steps: one forward over their P*S frames, then NMS and the P
+    steps' SORT + hand-back in step order (`chunk` counts units; the default
+    keeps 8 steps per graph).
+
     Each step's T stage ends with the result hand-back into that step's own
     pinned host record (outs[k]["record"]), so every outs[k] holds step k's
     detections and track ids after run(); outs[k]["proc"] is step k's proc
