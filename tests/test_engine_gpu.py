@@ -181,6 +181,9 @@ def test_bench_configuration_parity(cuda, depth, lanes, pair):
         chk.check(frames[f], out["proc"], eng.results(out), f / 30.0)
     eng.autotune(frames[0], reps=1)
     assert len(eng.detector.tuned_configs()) > 0
+    # bench.py's --conv-grid persistent: the tuned tiles on persistent grids
+    eng.detector.load_tuned([tuple(c[:4]) + (1,) + tuple(c[5:])
+                             for c in eng.detector.tuned_configs()])
     run = OverlappedSteps(eng, [frames[WARM + k] for k in range(K)],
                           [ts[WARM + k] for k in range(K)], depth=depth, chunk=8)
     run.run()
