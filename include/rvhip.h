@@ -476,10 +476,10 @@ int rv_capture_info(void* handle, int* info);
 int rv_capture_next(void* handle, uint8_t** frame, double* ts, int64_t* index, int* slot);
 int rv_capture_release(void* handle, int slot);
 /* One frame of each of S sources -> dev + s * dev_stride (H2D on `stream`);
- * each slot returns to its reader by a host callback queued behind its copy,
- * so the rings refill while the device works.  ts / index (host, S) may be
+ * each slot returns to its reader once an event recorded behind its copy has
+ * completed, so the rings refill while the device works.  ts / index (host, S) may be
  * NULL.  RV_EOF when a source ended (frames already queued are still
- * copied).  rv_capture_close waits for queued slot releases. */
+ * copied); rv_capture_close waits for copies still in flight. */
 int rv_capture_upload_batch(void* const* handles, int S, uint8_t* dev, size_t dev_stride,
                             double* ts, int64_t* index, void* stream);
 int rv_capture_close(void* handle);

@@ -8,18 +8,20 @@
 // consumer takes filled slots in order and hands them back when done.
 //
 // rv_capture_upload_batch feeds RoadVisionEngine: for S sources it takes one
-// frame of each, queues its H2D copy on the caller's stream and, behind the
-// copy in the same stream, a host callback that returns the slot to its
-// reader -- so the ring refills while the device works and nothing blocks on
-// the copy.  Frames travel as NV12 (1.5 B/pixel: what a decoder emits; the
+// frame of each, queues its H2D copy on the caller's stream and records an
+// event behind it; the slot returns to its reader once that event has
+// completed (polled at the next upload; waited for only when a source has
+// no other slot to hand out) -- so the ring refills while the device works
+// and nothing blocks on a copy in flight.  No host callbacks are queued in
+// streams.  Frames travel as NV12 (1.5 B/pixel: what a decoder emits; the
 // device converts with rv_nv12_to_bgr_u8) or as raw BGR.
 //
 // Formats: YUV4MPEG2 (.y4m, 4:2:0 planar, converted to NV12 by the reader
 // thread: U/V interleave), raw NV12, raw BGR.  There is no bitstream decoder
 // in this image (no rocDecode), and no V4L2 camera: DESIGN.md §(f)4.
-#include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -56,10 +58,13 @@ struct Capture {
   bool stop = false, eof = false;
   int err = RV_OK;
   int64_t count = 0;
-  // slot-release callbacks queued in streams and not yet finished: close
-  // waits for them (a stream can read as complete before its host function
-  // has returned), so no callback ever touches a freed Capture
-  std::atomic<int> pending{0};
+  // uploaded slots whose H2D copy may still be in flight (consumer side):
+  // the slot goes back to the reader when its event has completed
+  struct InFlight {
+    hipEvent_t ev;
+    int slot;
+  };
+  std::deque<InFlight> inflight;
 };
 
 double wall_now() {
@@ -175,17 +180,34 @@ void give_back(Capture* c, int slot) {
   c->cv_fill.notify_one();
 }
 
-struct Release {
-  Capture* c;
-  int slot;
-};
+// Return the slots whose copies have completed (all of them, waiting, with
+// `wait`); false if a wait failed.
+bool reap(Capture* c, bool wait) {
+  while (!c->inflight.empty()) {
+    Capture::InFlight& f = c->inflight.front();
+    const hipError_t e = wait ? hipEventSynchronize(f.ev) : hipEventQuery(f.ev);
+    if (e == hipErrorNotReady) return true;
+    (void)hipEventDestroy(f.ev);
+    give_back(c, f.slot);
+    c->inflight.pop_front();
+    if (e != hipSuccess) return false;
+  }
+  return true;
+}
 
-void release_cb(void* p) {
-  Release* r = static_cast<Release*>(p);
-  Capture* c = r->c;
-  give_back(c, r->slot);
-  delete r;
-  c->pending.fetch_sub(1);  // the last access to c
+// take() for the upload path: while the reader has nothing filled and every
+// other slot waits on a copy, wait for the oldest copy so the reader can
+// refill (no deadlock between a full ring and a blocked consumer).
+int take_for_upload(Capture* c, int* slot) {
+  reap(c, false);
+  for (;;) {
+    {
+      std::lock_guard<std::mutex> lk(c->m);
+      if (c->slots[c->tail].state == 1 || c->eof || c->inflight.empty()) break;
+    }
+    if (!reap(c, true)) break;
+  }
+  return take(c, slot);
 }
 
 }  // namespace
@@ -294,23 +316,26 @@ extern "C" int rv_capture_upload_batch(void* const* handles, int S, uint8_t* dev
     Capture* c = static_cast<Capture*>(handles[s]);
     RV_CHECK_ARG(c != nullptr && dev_stride >= c->frame_bytes, "stream %d: null or stride", s);
     int slot = -1;
-    const int rc = take(c, &slot);
-    if (rc != RV_OK) return rc;  // frames already queued return their slots by callback
+    const int rc = take_for_upload(c, &slot);
+    if (rc != RV_OK) return rc;  // frames already queued return their slots at the next reap
     if (ts) ts[s] = c->slots[slot].ts;
     if (index) index[s] = c->slots[slot].index;
     int e = hip_check(hipMemcpyAsync(dev + (size_t)s * dev_stride, c->slots[slot].p,
                                      c->frame_bytes, hipMemcpyHostToDevice, st),
                       "hipMemcpyAsync(capture)");
-    if (e == RV_OK) {
-      c->pending.fetch_add(1);
-      e = hip_check(hipLaunchHostFunc(st, release_cb, new Release{c, slot}),
-                    "hipLaunchHostFunc(capture release)");
-      if (e != RV_OK) c->pending.fetch_sub(1);
-    }
+    hipEvent_t ev = nullptr;
+    if (e == RV_OK)
+      e = hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate(capture)");
+    if (e == RV_OK) e = hip_check(hipEventRecord(ev, st), "hipEventRecord(capture)");
     if (e != RV_OK) {
+      if (ev) {
+        (void)hipStreamSynchronize(st);
+        (void)hipEventDestroy(ev);
+      }
       give_back(c, slot);
       return e;
     }
+    c->inflight.push_back({ev, slot});
   }
   return RV_OK;
 }
@@ -318,15 +343,7 @@ extern "C" int rv_capture_upload_batch(void* const* handles, int S, uint8_t* dev
 extern "C" int rv_capture_close(void* handle) {
   if (!handle) return RV_OK;
   Capture* c = static_cast<Capture*>(handle);
-  // queued slot releases first (bounded: 10 s, then the capture is leaked
-  // rather than freed under a callback)
-  for (int i = 0; c->pending.load() > 0; ++i) {
-    if (i == 100000) {
-      set_error("rv_capture_close: %d slot releases still queued", c->pending.load());
-      return RV_EINVAL;
-    }
-    std::this_thread::sleep_for(std::chrono::microseconds(100));
-  }
+  reap(c, true);  // copies still in flight read the slots: wait for them
   {
     std::lock_guard<std::mutex> lk(c->m);
     c->stop = true;
