@@ -15,8 +15,8 @@ image: they raise instead of falling back.
 
 ``MultiStreamCapture(sources, device)`` is the batched pipeline: for S
 sources, ``next_batch()`` queues one frame of each as an H2D copy on a copy
-stream (the slot goes back to its reader by a host callback queued behind
-the copy), converts the NV12 batch to BGR on the device, and prefetches the
+stream (the slot goes back to its reader once an event recorded behind the
+copy has completed; polled at the next upload), converts the NV12 batch to BGR on the device, and prefetches the
 next batch while the caller runs the current one (two device buffers).
 """
 from __future__ import annotations

@@ -1,7 +1,7 @@
 """Capture front end on the GPU: frames read by the native reader threads,
 uploaded as NV12 and converted on the device equal the C oracle's
 cv2.COLOR_YUV2BGR_NV12 of the same bytes, bit for bit; the batched pipeline
-(MultiStreamCapture: copy stream, host-callback slot release, one batch of
+(MultiStreamCapture: copy stream, event-polled slot release, one batch of
 prefetch) keeps every stream's frames in order and feeds RoadVisionEngine."""
 import numpy as np
 import pytest
