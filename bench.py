@@ -6,22 +6,33 @@ MI355X: CLAHE+Median+YOLOv8n+NMS+SORT IoU".  A step = one pass of the hot path
 over one stream-major batch (32 camera streams x 1 frame): fused CLAHE+median
 (proc frames written to HBM), letterbox, YOLOv8n forward (bf16 MFMA), NMS +
 scale_boxes + class filter, SORT (KF + IoU + greedy association) with
-ground-plane homography metrics, and the hand-back of the step's detections,
-track ids and metrics to pinned host memory (the reference's .cpu().numpy(),
-src/detect/yolo_ultralytics.py:44-52).  Inputs are synthetic road frames
-generated on the device before the timed region (resident in HBM).
+ground-plane homography metrics, the hand-back of the step's detections,
+track ids and metrics to pinned host memory, and -- on a consumer thread
+inside the timed region -- the reference's List[Detection] of every stream
+(src/detect/yolo_ultralytics.py:44-52, src/track/sort_tracker.py:278).
+Inputs are synthetic road frames generated on the device before the timed
+region (resident in HBM).
 
-Multi-GPU (torchrun, one process per GPU): camera streams are sharded
-(stream s -> rank s // 32), no collective on the data path (weak scaling);
-rank timings are reduced with a MAX for the reported time (rvs_amd.shard:
-init_from_env, timed_job -- the same code the gloo test drives on the CPU).
+The K steps run as the 4-stage software pipeline of rvs_amd.schedule
+(PipelinedRun: native launch list over four HIP streams, no graph capture).
+
+Multi-GPU: one process per GPU.  Under torchrun the rank comes from the
+environment; ``--gpus N`` without it spawns the N ranks itself (fresh child
+processes, before this process touches the GPU).  Camera streams are
+sharded (stream s -> rank s // 32), no collective on the data path (weak
+scaling); rank timings are reduced with a MAX (rvs_amd.shard.timed_job).
 
 Prints ONE JSON line (rank 0).
 """
 import argparse
+import hashlib
+import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -40,7 +51,8 @@ PEAK_HBM = 8000.0                      # GB/s
 IMAGE_POINTS = [[560, 1000], [1360, 1000], [1160, 620], [760, 620]]
 WORLD_POINTS = [[-3.5, 5.0], [3.5, 5.0], [3.5, 30.0], [-3.5, 30.0]]
 METRIC = "end-to-end frames/sec @1080p (preproc+YOLOv8n+SORT), 1/2/4/8 MI355X"
-PMC_TRAFFIC = os.path.join(REPO, "profiles", "r02", "pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "r03", "pmc_traffic.json")
+LIB = os.path.join(REPO, "road-vision-system_amd", "rvs_amd", "librvhip.so")
 
 
 def bench_config():
@@ -56,43 +68,45 @@ def bench_config():
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60)  # pipeline fill/drain < 1 %
+    ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--streams", type=int, default=32, help="camera streams per GPU")
     ap.add_argument("--tmax", type=int, default=int(os.environ.get("RV_TMAX", 1024)),
                     help="SORT track capacity per stream")
-    ap.add_argument("--cpu-frames", type=int, default=int(os.environ.get("RV_CPU_FRAMES", 30)))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--eager", action="store_true", help="launch kernels eagerly (no HIP graph)")
+    ap.add_argument("--exec", dest="exec_mode", choices=["native", "eager", "sequential"],
+                    default=os.environ.get("RV_EXEC", "native"),
+                    help="the pipelined schedule issued by the native launch list (one C call "
+                         "per run) or eagerly from Python; or plain sequential step() calls")
+    ap.add_argument("--sync", choices=["flow", "stage"], default=os.environ.get("RV_SYNC", "flow"),
+                    help="pipeline dependencies: per-dependency events (flow) or lock-stepped "
+                         "stages (stage)")
+    ap.add_argument("--pair", type=int, default=int(os.environ.get("RV_PAIR", 4)),
+                    help="steps per pipeline unit (one forward over pair x streams frames); the "
+                         "largest divisor of --steps not above it is used")
+    ap.add_argument("--no-consumer", action="store_true",
+                    help="do not build the Detection lists inside the timed region")
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip the per-layer conv kernel autotuning before the timed region")
     ap.add_argument("--conv-grid", choices=["persistent", "tuned"],
                     default=os.environ.get("RV_CONV_GRID", "persistent"),
-                    help="pipelined runs: keep the autotuned tile of every conv launch but run it "
-                         "on a persistent grid (default), or keep the autotuner's grid choice")
+                    help="keep the autotuned tile of every conv launch but run it on a "
+                         "persistent grid (default), or keep the autotuner's grid choice")
     ap.add_argument("--tune-save", default=None, help="write the autotuned conv configs (JSON)")
     ap.add_argument("--tune-load", default=None,
                     help="load conv configs saved by --tune-save instead of autotuning")
     ap.add_argument("--conv-timing", choices=["both", "overlap", "eager", "none"], default="both",
-                    help="per-launch conv timing after the timed region: HIP events around "
-                         "every conv launch while the timed region's multi-stream schedule runs "
-                         "eagerly (overlap: same concurrency as the graphs), a plain sequential "
-                         "eager pass, or none")
-    ap.add_argument("--depth", type=int, default=int(os.environ.get("RV_PIPE_DEPTH", 4)),
-                    help="pipelined steps: 4 = Y2(k-1) || P(k+1) || Y1(k) || T(k-2) (the forward "
-                         "split in two halves on two forward lanes), 3 = Y(k) || P(k+1) || T(k-1), "
-                         "2 = [T(k-1) || P(k)] -> Y(k)")
-    ap.add_argument("--graph-chunk", type=int, default=None,
-                    help="pipeline steps per captured graph (default 8, RV_GRAPH_CHUNK; 0 = all)")
-    ap.add_argument("--pair", type=int, default=int(os.environ.get("RV_PAIR", 4)),
-                    help="depth 4: run the forwards of this many consecutive steps as one batch "
-                         "(pair x streams frames; SORT still sees every stream in order); the "
-                         "largest divisor of --steps not above it is used")
-    ap.add_argument("--lanes", type=int, default=int(os.environ.get("RV_LANES", 1)),
-                    help="forward lanes: the YOLO forwards of this many consecutive steps run "
-                         "concurrently (engine.OverlappedSteps dependency-graph schedule)")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="one graph per step; no overlap of step k's NMS+SORT with step k+1")
+                    help="per-launch conv timing after the timed region (HIP events around every "
+                         "conv launch): the timed region's schedule issued eagerly (overlap), one "
+                         "unit at a time with each launch alone (eager), both, or none")
+    ap.add_argument("--cpu-frames", type=int, default=int(os.environ.get("RV_CPU_FRAMES", 12)),
+                    help="CPU baseline: frames per worker (one camera stream per worker)")
+    ap.add_argument("--cpu-workers", type=int, default=int(os.environ.get("RV_CPU_WORKERS", 0)),
+                    help="CPU baseline workers (0: OMP_NUM_THREADS, else the CPUs this process "
+                         "may run on)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--job", default=None,
+                    help="module:Class of a stand-in rank job (CPU rehearsal of the rank logic "
+                         "with gloo; tests/test_shard_gloo.py)")
     return ap.parse_args(argv)
 
 
@@ -100,6 +114,28 @@ def pick_pair(steps: int, pair: int) -> int:
     """Steps per pipeline unit: the largest p <= pair that divides `steps`
     (a driver may pass any --steps)."""
     return max(p for p in range(1, max(1, pair) + 1) if steps % p == 0)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """`--gpus N` without a torchrun environment: start N fresh ranks of this
+    script (rank r on GPU r, torchrun's variables), wait for all of them and
+    return the worst exit code.  Called before anything touches the GPU."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    codes = [p.wait() for p in procs]
+    return max(codes, key=abs)
 
 
 class BenchJob:
@@ -112,11 +148,8 @@ class BenchJob:
         self.args, self.dev = args, dev
         self.cfg = bench_config()
         self.S, self.K, self.Wm = args.streams, args.steps, args.warmup
-        # depth 4 runs the two halves of consecutive forwards on two lanes
-        lanes = 2 if args.depth == 4 and not args.no_pipeline and not args.eager else args.lanes
-        pair = 1
-        if args.depth == 4 and not args.no_pipeline and not args.eager:
-            pair = pick_pair(args.steps, args.pair)
+        seq = args.exec_mode == "sequential"
+        lanes, pair = (1, 1) if seq else (2, pick_pair(args.steps, args.pair))
         self.eng = RoadVisionEngine(self.cfg, self.S, (H, W), device=dev, tmax=args.tmax,
                                     lanes=lanes, pair=pair)
         self.frames = road_frames(self.S, self.Wm + self.K, H, W, device=dev,
@@ -124,12 +157,21 @@ class BenchJob:
         self.ts = torch.tensor([[f / 30.0] * self.S for f in range(self.Wm + self.K)],
                                dtype=torch.float64, device=dev)
         self.units = self.S * self.K
-        self.runner = self.graphs = None
+        self.runner = None
+        # host thread during the timed region: "consume" builds every step's
+        # Detection lists, "watch" only notes when each step was handed back
+        self.consume = "off" if args.no_consumer else "consume"
+        self._consumer = None
+        self.cons = {}
+        self.records = None
+        self.device_end = 0.0
         torch.cuda.synchronize()
 
     def warmup(self):
         for f in range(self.Wm):
-            self.eng.step(self.frames[f], self.ts[f])
+            out = self.eng.step(self.frames[f], self.ts[f])
+        if self.Wm:
+            self.eng.results(out)
         torch.cuda.synchronize()
 
     def prepare(self):
@@ -139,10 +181,10 @@ class BenchJob:
                 eng.detector.load_tuned([tuple(c) for c in json.load(f)["configs"]])
         elif not a.no_autotune:  # per-layer conv kernel choice, on real activations
             eng.autotune(self.frames[0], reps=int(os.environ.get("RV_AUTOTUNE_REPS", "10")))
-            if a.conv_grid == "persistent" and not a.eager and not a.no_pipeline:
+            if a.conv_grid == "persistent" and a.exec_mode != "sequential":
                 # every conv on a persistent grid: the autotuner times each
-                # launch alone, but inside the pipelined graphs persistent
-                # grids share the chip better (A/B: +0.6 %)
+                # launch alone, but beside the other pipeline stages persistent
+                # grids share the chip better
                 eng.detector.load_tuned([tuple(c[:4]) + (1,) + tuple(c[5:])
                                          for c in eng.detector.tuned_configs()])
             if a.tune_save:
@@ -150,16 +192,33 @@ class BenchJob:
                     json.dump({"configs": eng.detector.tuned_configs()}, f)
         torch.cuda.synchronize()
         K, Wm = self.K, self.Wm
-        if not a.eager and not a.no_pipeline:
-            from rvs_amd.engine import OverlappedSteps
-            # NMS + SORT + hand-back of step k overlap the preprocess of step k+1
-            # and the forward of step k+1 runs beside both (engine.OverlappedSteps)
-            self.runner = OverlappedSteps(eng, [self.frames[Wm + k] for k in range(K)],
-                                          [self.ts[Wm + k] for k in range(K)], depth=a.depth,
-                                          chunk=a.graph_chunk)
-        elif not a.eager:
-            self.graphs = [eng.capture(self.frames[Wm + k], self.ts[Wm + k])[0] for k in range(K)]
+        if a.exec_mode == "sequential":
+            from rvs_amd.handback import Record
+            self.records = [Record(self.S, eng.detector.max_det, self.dev) for _ in range(K)]
+        else:
+            from rvs_amd.schedule import PipelinedRun
+            self.runner = PipelinedRun(eng, [self.frames[Wm + k] for k in range(K)],
+                                       [self.ts[Wm + k] for k in range(K)], mode=a.exec_mode,
+                                       sync=a.sync)
+            self.records = self.runner.records
         torch.cuda.synchronize()
+
+    def _consume(self, wait_step, materialise: bool):
+        """The consumer: every step's List[Detection] per stream, built as
+        soon as that step's record has been handed back (materialise=False:
+        only the host time each step became available)."""
+        from rvs_amd.handback import to_detections
+        names, n_det, busy, done = self.eng.names, 0, 0.0, []
+        for k, rec in enumerate(self.records):
+            wait_step(k)
+            t = time.perf_counter()
+            done.append(t)
+            if materialise:
+                n, rows = rec.arrays()
+                n_det += sum(len(x) for x in to_detections(n, rows, names))
+                busy += time.perf_counter() - t
+        self.cons = {"detections": n_det, "busy_s": busy, "end": time.perf_counter(),
+                     "done": done}
 
     def run(self):
         from rvs_amd import _lib
@@ -167,34 +226,27 @@ class BenchJob:
         _lib.call("rv_trace_marker", 1, st)  # brackets the timed region in a kernel trace
         if self.runner is not None:
             self.runner.run()
+            wait = self.runner.wait_step
         else:
+            evs = []
             for k in range(self.K):
-                if self.graphs is not None:
-                    self.graphs[k].replay()
-                else:
-                    self.eng.step(self.frames[self.Wm + k], self.ts[self.Wm + k])
+                self.eng.step(self.frames[self.Wm + k], self.ts[self.Wm + k], self.records[k])
+                e = torch.cuda.Event()
+                e.record()
+                evs.append(e)
+            wait = lambda k: evs[k].synchronize()  # noqa: E731
         _lib.call("rv_trace_marker", 2, st)
+        if self.consume != "off":
+            self._consumer = threading.Thread(target=self._consume,
+                                              args=(wait, self.consume == "consume"))
+            self._consumer.start()
 
-    @staticmethod
-    def sync():
+    def sync(self):
         torch.cuda.synchronize()
-
-    def materialise(self) -> dict:
-        """Detection-list construction from the handed-back host records of
-        the timed steps (host work after the hand-back; reported separately)."""
-        from rvs_amd.handback import to_detections
-        if self.runner is None:
-            return {"in_timed_region": True, "materialise_ms_per_step": None}
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        nd = 0
-        for rec in self.runner.records:
-            n, rows = rec.arrays()
-            nd += sum(len(x) for x in to_detections(n, rows, self.eng.names))
-        dt = time.perf_counter() - t0
-        return {"in_timed_region": True, "record_bytes_per_step": self.runner.records[0].nbytes,
-                "detections_per_step": round(nd / self.K, 1),
-                "materialise_ms_per_step": round(dt / self.K * 1e3, 3)}
+        self.device_end = time.perf_counter()
+        if self._consumer is not None:
+            self._consumer.join()
+            self._consumer = None
 
     def track_report(self) -> dict:
         st = self.eng.track_stats()
@@ -203,21 +255,33 @@ class BenchJob:
 
 
 def rank_job(job, device) -> dict:
-    """warm-up, preparation (autotune + capture), then the timed region
-    (rvs_amd.shard.timed_job: barrier, sync, K steps, sync, max over ranks)."""
+    """warm-up, preparation (autotune + the recorded schedule), then the
+    timed region (rvs_amd.shard.timed_job: barrier, sync, K steps, sync, max
+    over ranks)."""
     from rvs_amd.shard import timed_job
     job.warmup()
     job.prepare()
     return timed_job(job.run, job.sync, job.units, device)
 
 
+def rank_job_again(job, device) -> dict:
+    """A second timed region over the same recorded schedule, without the
+    Detection lists (a watcher thread only notes each step's completion)."""
+    from rvs_amd.shard import timed_job
+    consume, job.consume = job.consume, "watch"
+    try:
+        return timed_job(job.run, job.sync, job.units, device)
+    finally:
+        job.consume = consume
+
+
 def _conv_pass(job, mode: str, tags):
     """One profiled pass over the K steps: HIP events around every conv
     launch of lane 0's forwards (rv_yolo_profile), bracketed by trace
     markers `tags` so tools/trace_window.py can cut the same window out of
-    a rocprofv3 trace.  Returns (ms per forward, FLOPs, bytes, launches)."""
+    a rocprofv3 trace.  Returns (ms per step, FLOPs, bytes, launches)."""
     from rvs_amd import _lib
-    from rvs_amd.engine import OverlappedSteps
+    from rvs_amd.schedule import PipelinedRun
     eng, K, Wm = job.eng, job.K, job.Wm
     lib = _lib.load()
     h = eng.detector._h
@@ -226,11 +290,10 @@ def _conv_pass(job, mode: str, tags):
     _lib.check(lib.rv_yolo_profile_reps(h, K, 5 if mode == "eager" else 1), "rv_yolo_profile")
     st = _lib.stream_ptr()
     _lib.call("rv_trace_marker", tags[0], st)
-    prof = None
-    if mode == "overlap":
-        prof = OverlappedSteps(eng, [job.frames[Wm + k] for k in range(K)],
-                               [job.ts[Wm + k] for k in range(K)], depth=job.args.depth,
-                               chunk=job.args.graph_chunk, capture=False)
+    if mode == "overlap":  # the timed region's schedule, issued eagerly with the events
+        prof = PipelinedRun(eng, [job.frames[Wm + k] for k in range(K)],
+                            [job.ts[Wm + k] for k in range(K)], mode="eager", sync=job.args.sync)
+        prof.run()
     elif eng.pair > 1:  # each launch alone, on the timed region's forward batch
         from rvs_amd.handback import Record
         P = eng.pair
@@ -248,59 +311,68 @@ def _conv_pass(job, mode: str, tags):
     cv = np.zeros(n, np.int32)
     nf = lib.rv_yolo_profile_read(h, ms.ctypes.data, fl.ctypes.data, cv.ctypes.data, n)
     lib.rv_yolo_profile_bytes(h, by.ctypes.data, n)
-    prof = None  # noqa: F841 -- eager schedule objects before the events
     torch.cuda.synchronize()
     lib.rv_yolo_profile(h, 0)
     valid = cv >= 0
-    # pair mode: every profiled forward covers `pair` steps -> per step
+    # every profiled forward covers `pair` steps -> per step
     per = eng.pair
     return (float(ms[valid].sum()) / max(nf, 1) / per, float(fl[valid].sum()) / per,
             float(by[valid].sum()) / per, int(valid.sum()) / per)
 
 
+def _lib_sha256() -> str:
+    with open(LIB, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def pmc_traffic() -> dict:
+    """HBM bytes per step of the conv family from rocprofv3 PMC passes
+    (tools/gpu_pmc.sh -> profiles/r03/pmc_traffic.json), reported only when
+    they were collected on the library this run loaded (same sha256)."""
+    if not os.path.exists(PMC_TRAFFIC):
+        return {"traffic": None, "traffic_note": "no PMC pass of this round's library"}
+    d = json.load(open(PMC_TRAFFIC))
+    if d.get("librvhip_sha256") != _lib_sha256():
+        return {"traffic": None,
+                "traffic_note": "the PMC passes in profiles/r03/pmc_traffic.json were collected "
+                                "on another build of librvhip.so: not reported"}
+    return {"traffic": d.get("conv_bytes_per_step"),
+            "traffic_unit": "HBM bytes per step, all conv launches (rocprofv3 PMC: 2 x "
+                            "FETCH_SIZE + WRITE_SIZE, separate passes, this build; "
+                            "profiles/r03/pmc_traffic.json)"}
+
+
 def conv_roofline(job, mode: str) -> dict:
     """Roofline of the conv family (every conv launch of a step:
-    conv_patch_kernel, conv1x1_direct_kernel, c2f_chain_kernel) from HIP
-    events recorded on the launch stream around every conv launch
-    (rv_yolo_profile; HIP events recorded inside captured graphs read zero
-    elapsed time on ROCm 7.2, so the timed graphs themselves cannot be timed
-    this way).  achieved = algorithmic bytes (or FLOPs) of the family per
-    step / its measured time per step.
-      "eager": one step at a time, each launch alone, five times back to
-               back between its events -- the kernels' own speed (the
-               headline `roofline`; rocprofv3 cross-check: the trace window
-               between the 5th and 6th rv_trace_marker);
-      "overlap": the timed region's multi-stream schedule run eagerly, so
-               each launch sees the concurrency it sees inside the timed
-               graphs (`in_pipeline`; window: markers 3 and 4).
-    "both" measures both."""
-    eng = job.eng
-    job.runner = None  # release the timed graphs (and their memory pool) first
+    conv_patch_kernel, conv1x1_direct_kernel, c2f_chain_kernel) against
+    SURVEY §8(d)'s MFMA bound: achieved = the family's algorithmic FLOPs per
+    step / its HIP-event-timed duration per step (rv_yolo_profile: events on
+    the launch stream around every conv launch).
+      "eager": one pipeline unit at a time, each launch alone, five times
+               back to back between its events -- the kernels' own speed
+               (the headline; rocprofv3 cross-check: trace window between
+               the 5th and 6th rv_trace_marker);
+      "overlap": the timed region's schedule issued eagerly, so each launch
+               sees the concurrency it has in the timed region
+               (`in_pipeline`; window: markers 3 and 4).
+    The bytes view (algorithmic activation + weight bytes of the launches at
+    8 TB/s) is reported beside it."""
+    job.runner = None
     torch.cuda.synchronize()
-    torch.cuda.empty_cache()
     res = {}
     for m, tags in (("overlap", (3, 4)), ("eager", (5, 6))):
         if mode in (m, "both"):
             res[m] = _conv_pass(job, m, tags)
-    traffic = None
-    if os.path.exists(PMC_TRAFFIC):
-        traffic = json.load(open(PMC_TRAFFIC)).get("conv_bytes_per_step")
 
     def view(conv_ms, flop, byts, nl):
         tflops = flop / (conv_ms * 1e-3) / 1e12
         gbs = byts / (conv_ms * 1e-3) / 1e9
-        # which roofline binds the conv family: its algorithmic bytes at peak
-        # HBM vs its FLOPs at peak bf16 MFMA (small channel counts: bytes win)
-        hbm = byts / (PEAK_HBM * 1e9) >= flop / (PEAK_BF16 * 1e12)
-        return {"bound": "hbm" if hbm else "mfma",
-                "achieved": round(gbs if hbm else tflops, 2),
-                "peak": PEAK_HBM if hbm else PEAK_BF16,
-                "unit": "GB/s" if hbm else "TFLOP/s",
-                "frac": round(gbs / PEAK_HBM if hbm else tflops / PEAK_BF16, 5),
-                "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / PEAK_BF16, 5),
-                "hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / PEAK_HBM, 5),
+        return {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16,
+                "unit": "TFLOP/s", "frac": round(tflops / PEAK_BF16, 5),
+                "bytes_view": {"achieved_gbs": round(gbs, 1), "peak_gbs": PEAK_HBM,
+                               "frac": round(gbs / PEAK_HBM, 5),
+                               "algorithmic_bytes_per_step": round(byts)},
                 "launches_per_step": nl, "conv_ms_per_step": round(conv_ms, 4),
-                "algorithmic_bytes_per_step": round(byts),
                 "algorithmic_gflop_per_step": round(flop / 1e9, 2)}
     if not res or any(v[0] <= 0 for v in res.values()):
         return {"error": "no event timings"}
@@ -309,16 +381,13 @@ def conv_roofline(job, mode: str) -> dict:
                      "(all YOLOv8n conv launches of a step; HIP events on the launch stream)",
            "timing": main + (" (one pipeline unit at a time: each launch alone, on the timed "
                              "region's forward batch)" if main == "eager" else
-                             " (the timed region's schedule run eagerly)")}
+                             " (the timed region's schedule issued eagerly)")}
     out.update(view(*res[main]))
-    out["traffic"] = traffic
-    out["traffic_unit"] = ("bytes per step (all conv launches; rocprofv3 PMC 2 x FETCH_SIZE + "
-                           "WRITE_SIZE, separate passes over one eager step; "
-                           "profiles/r02/pmc_traffic.json)")
+    out.update(pmc_traffic())
     if main == "eager" and "overlap" in res:
         out["in_pipeline"] = dict(view(*res["overlap"]), timing=(
-            "the timed region's schedule run eagerly: each conv launch timed under the "
-            "concurrency it has inside the timed graphs"))
+            "the timed region's schedule issued eagerly: each conv launch timed under the "
+            "concurrency it has in the timed region"))
     return out
 
 
@@ -332,18 +401,18 @@ def host_cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(frames_host: np.ndarray, ts: np.ndarray, cfg: dict, threads: int) -> dict:
-    """The CPU oracle port of the reference path timed on this host's cores:
-    C restatement of CLAHE/median/letterbox (OpenMP over `threads`), torch-CPU
-    fp32 YOLOv8n (batch 1, `threads` intra-op threads), restated NMS,
-    reference-semantics Python SORT + homography -- frame by frame, as
-    main_preview.py:94-109 runs it.  Plus the reference's SORT association
-    alone (_iou_matrix Python double loop + greedy, sort_tracker.py:182-210)
-    at T = D = 100."""
+def _cpu_worker(wid: int, nfr: int, cfg: dict, start, q):
+    """One camera stream on one core: the oracle port of the reference chain
+    frame by frame, single-threaded, as main_preview.py:94-109 runs it: C
+    restatement of CLAHE/median/letterbox, torch-CPU fp32 YOLOv8n, restated
+    NMS, reference-semantics Python SORT + homography."""
+    os.environ["OMP_NUM_THREADS"] = "1"
+    torch.set_num_threads(1)
     from oracle import cpu, sort_ref, yolo_ref
     from rvs_amd.detect.weights import synthetic_weights
     from rvs_amd.geometry import find_homography
-    torch.set_num_threads(threads)  # also the OpenMP team of the C oracle
+    from rvs_amd.synth import road_frames
+    frames = road_frames(1, nfr, H, W, device="cpu", stream_offset=wid)[:, 0].numpy()
     model = yolo_ref.YoloRef(0, synthetic_weights(0, 0))
     proj = sort_ref.HomographyProjector(find_homography(np.array(IMAGE_POINTS, np.float32),
                                                         np.array(WORLD_POINTS, np.float32)),
@@ -352,9 +421,9 @@ def cpu_baseline(frames_host: np.ndarray, ts: np.ndarray, cfg: dict, threads: in
     geo = cpu.letterbox_geometry(H, W)
     keep = cfg["detect"]["classes_keep"]
     stage = np.zeros(4)
+    start.wait()
     t0 = time.perf_counter()
-    n = 0
-    for img, t in zip(frames_host, ts):
+    for f, img in enumerate(frames):
         a = time.perf_counter()
         proc = cpu.median(cpu.clahe_ycrcb(img, 8, 2.0), 3)
         lb = cpu.letterbox(proc, geo)[None]
@@ -363,12 +432,33 @@ def cpu_baseline(frames_host: np.ndarray, ts: np.ndarray, cfg: dict, threads: in
         c = time.perf_counter()
         dets = yolo_ref.postprocess(raw, geo[:2], (H, W), classes_keep=keep)[0]
         d = time.perf_counter()
-        trk.update([sort_ref.Det(*map(float, r[:5]), int(r[5])) for r in dets], float(t), proj)
+        trk.update([sort_ref.Det(*map(float, r[:5]), int(r[5])) for r in dets], f / 30.0, proj)
         e = time.perf_counter()
         stage += [b - a, c - b, d - c, e - d]
-        n += 1
-    dt = time.perf_counter() - t0
-    # the reference's association at T = D = 100 (72.9 ms on the container Xeon)
+    q.put((wid, len(frames), time.perf_counter() - t0, stage.tolist()))
+
+
+def cpu_baseline(cfg: dict, nfr: int, workers: int) -> dict:
+    """The CPU oracle port of the reference path on this host: `workers`
+    processes, one camera stream each on one core (streams are independent,
+    SURVEY §8(e)), released together after each has built its frames and
+    model; value = all frames / the slowest worker's time.  Plus the
+    reference's SORT association alone (_iou_matrix Python double loop +
+    greedy, sort_tracker.py:182-210) at T = D = 100."""
+    import multiprocessing as mp
+    from oracle import sort_ref
+    ctx = mp.get_context("spawn")  # fresh interpreters: nothing GPU-side is inherited
+    start, q = ctx.Event(), ctx.Queue()
+    procs = [ctx.Process(target=_cpu_worker, args=(w, nfr, cfg, start, q)) for w in range(workers)]
+    for p in procs:
+        p.start()
+    start.set()  # each worker times only its own frame loop (after its setup)
+    res = [q.get(timeout=900) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    frames = sum(r[1] for r in res)
+    slowest = max(r[2] for r in res)
+    stage = np.sum([r[3] for r in res], axis=0) / frames
     rng = np.random.default_rng(0)
     xy = rng.uniform(0, 1800, (100, 2)).astype(np.float32)
     wh = rng.uniform(20, 200, (100, 2)).astype(np.float32)
@@ -379,23 +469,63 @@ def cpu_baseline(frames_host: np.ndarray, ts: np.ndarray, cfg: dict, threads: in
     for _ in range(reps):
         sort_ref.greedy(sort_ref.iou_matrix(tb, db), cfg["tracking"]["iou_threshold"])
     assoc_ms = (time.perf_counter() - a) / reps * 1e3
-    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "host_cpus": os.cpu_count(), "cpu_model": host_cpu_model(),
-            "torch_threads": torch.get_num_threads(),
-            "stage_ms_per_frame": {k: round(v / n * 1e3, 2) for k, v in
+    return {"value": frames / slowest, "unit": "frames/s", "cores": workers, "kind": "port",
+            "host_cpus": os.cpu_count(), "cpus_allowed": len(os.sched_getaffinity(0)),
+            "cpu_model": host_cpu_model(),
+            "per_core_frames_per_s": round(frames / sum(r[2] for r in res), 3),
+            "stage_ms_per_frame": {k: round(v * 1e3, 2) for k, v in
                                    zip(["preprocess+letterbox", "yolov8n_fp32", "nms",
                                         "sort+homography"], stage)},
             "sort_associate_ms_T100_D100": round(assoc_ms, 2),
-            "sample": f"{n} consecutive 1080p frames of one stream, full chain (C oracle "
-                      f"CLAHE+median+letterbox on {threads} OpenMP threads, torch-CPU fp32 "
-                      f"YOLOv8n {threads} threads, restated NMS, Python SORT+homography); "
-                      f"{dt:.1f} s"}
+            "sample": f"{workers} camera streams x {nfr} consecutive 1080p frames, one stream "
+                      f"per worker process on one core (C oracle CLAHE+median+letterbox, "
+                      f"torch-CPU fp32 YOLOv8n, restated NMS, Python SORT+homography; 1 thread "
+                      f"each); slowest worker {slowest:.1f} s"}
+
+
+def steady_state(job) -> dict:
+    """The steady-state rate of the last (device-only) run: host times at
+    which the watcher saw each step handed back, from the last step of the
+    second pipeline unit (the pipeline is full) to the last step -- beside
+    the fill-and-drain rate of the timed region."""
+    done = job.cons.get("done")
+    P = job.eng.pair
+    k0 = 2 * P - 1
+    if not done or len(done) - 1 <= k0:
+        return {}
+    per = (done[-1] - done[k0]) / (len(done) - 1 - k0)
+    return {"steady_state_ms_per_step": round(per * 1e3, 4),
+            "steady_state_frames_per_s": round(job.S / per, 1),
+            "steady_state_window": f"hand-back completions of steps {k0}..{len(done) - 1} of the "
+                                   "device-only run (host clock, watcher thread)"}
+
+
+def _stub_main(args, rank, world) -> None:
+    """Rank logic with a stand-in job (CPU rehearsal with gloo)."""
+    mod, cls = args.job.split(":")
+    job = getattr(importlib.import_module(mod), cls)(args, rank, "cpu")
+    t = rank_job(job, "cpu")
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": t["value"], "unit": "frames/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": t["elapsed_s"] / args.steps * 1e3,
+                          "world_size": torch.distributed.get_world_size()
+                          if torch.distributed.is_initialized() else 1,
+                          "local_s": t["local_s"], "elapsed_s": t["elapsed_s"]}), flush=True)
 
 
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus, argv)
     from rvs_amd.shard import init_from_env
-    rank, world, local = init_from_env("nccl")
+    rank, world, local = init_from_env("gloo" if args.job else "nccl")
+    if args.job:
+        _stub_main(args, rank, world)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -403,17 +533,28 @@ def main(argv=None):
     t = rank_job(job, dev)
     elapsed, value = t["elapsed_s"], t["value"]
     K, S = job.K, job.S
-    handback = job.materialise()
+    cons = job.cons
+    handback = {"consumer": ("in the timed region: a host thread builds every step's "
+                             "List[Detection] per stream (rvs_amd.handback.to_detections) as "
+                             "soon as the step's record is handed back"
+                             if job.consume == "consume" else "off"),
+                "record_bytes_per_step": job.records[0].nbytes}
+    if job.consume == "consume" and cons:
+        handback["detections_per_step"] = round(cons["detections"] / K, 1)
+        handback["materialise_ms_per_step"] = round(cons["busy_s"] / K * 1e3, 3)
+        handback["consumer_done_after_device_ms"] = round((cons["end"] - job.device_end) * 1e3, 3)
+    # the same K steps again without the consumer: the device-only rate, and
+    # the steady state from its per-step completion events
+    t2 = rank_job_again(job, dev) if job.consume == "consume" else None
+    steady = steady_state(job)
     sort_rep = job.track_report()
     roof = conv_roofline(job, args.conv_timing) if args.conv_timing != "none" else None
-
     P = job.eng.pair
-    if args.graph_chunk is not None:
-        chunk_desc = args.graph_chunk
-    else:
-        chunk_desc = int(os.environ.get("RV_GRAPH_CHUNK", "8"))
-        chunk_desc = max(1, chunk_desc // P) if chunk_desc > 0 and P > 1 else chunk_desc
-    chunk_desc = "all" if chunk_desc <= 0 else str(chunk_desc)
+    execution = ("sequential step() calls (no pipelining)" if args.exec_mode == "sequential" else
+                 f"{args.exec_mode} launch list (rvs_amd.schedule.PipelinedRun, sync={args.sync}):"
+                 f" 4-stage software pipeline over units of {P} steps -- second half of unit "
+                 "u-1's forward || preprocess of unit u+1 || first half of unit u's forward || "
+                 "NMS+SORT+hand-back of unit u-2 -- on 4 HIP streams, one C call per run")
     res = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -430,46 +571,39 @@ def main(argv=None):
                 "synthetic calibrated YOLOv8n weights (no checkpoint available)",
         "config": {"workload": "full chain 1920x1080, 32 camera streams x 1 frame per step per GPU: "
                                "CLAHE+Median (fused) -> letterbox -> YOLOv8n -> NMS -> "
-                               "SORT+homography -> result hand-back to pinned host memory",
+                               "SORT+homography -> result hand-back to pinned host memory -> "
+                               "List[Detection] per stream",
                    "streams_per_gpu": S, "frame": [H, W],
                    "detector_input": [job.eng.detector.in_h, job.eng.detector.in_w],
                    "parallelism": f"streams sharded {S}/GPU, no collective",
-                   "forward_batch": S * job.eng.pair,
-                   "conv_autotune": ("loaded" if args.tune_load else
-                                     (not args.no_autotune)),
+                   "forward_batch": S * P,
+                   "conv_autotune": ("loaded" if args.tune_load else (not args.no_autotune)),
                    "conv_grid": args.conv_grid,
-                   "execution": "eager" if args.eager else
-                                ("graph per step" if args.no_pipeline else
-                                 ("graphs, 4-stage software pipeline: stage k runs the second "
-                                  "half of unit k-1's forward || preprocess of unit k+1 || the "
-                                  "first half of unit k's forward || NMS+SORT+hand-back of unit "
-                                  f"k-2 (two forward workspaces; a unit = {job.eng.pair} step(s), "
-                                  f"one forward over their {S * job.eng.pair} frames), "
-                                  f"{chunk_desc} units per graph"
-                                  if args.depth == 4 else
-                                  f"graphs, dependency-graph pipeline with {args.lanes} concurrent "
-                                  "YOLO forwards (preprocess runs ahead, NMS+SORT+hand-back "
-                                  f"follows in step order), {chunk_desc} steps per graph"
-                                  if args.lanes > 1 else
-                                  f"graphs, {args.depth}-stage software pipeline over steps "
-                                  "(preprocess / YOLO / NMS+SORT+hand-back of consecutive steps "
-                                  f"overlap), {chunk_desc} steps per graph"))},
+                   "execution": execution},
+        "world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized()
+        else 1,
         "roofline": roof,
         "end_to_end_roofline_frac": round(value / world * (BYTES_PER_FRAME / (PEAK_HBM * 1e9) +
                                                            FLOP_PER_FRAME / (PEAK_BF16 * 1e12)), 5),
         "sort": sort_rep,
         "handback": handback,
     }
+    if t2 is not None:
+        res["device_only"] = {"value": round(t2["value"], 2),
+                              "ms_per_step": round(t2["elapsed_s"] / K * 1e3, 4),
+                              "note": "the same K steps timed again without the Detection "
+                                      "consumer (SORT continues from the first run)"}
+    res.update(steady)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0:
-        nfr = args.cpu_frames
-        host = job.frames[:nfr, 0].cpu().numpy()
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        res["cpu_baseline"] = cpu_baseline(host, np.arange(nfr) / 30.0, job.cfg, threads)
+        workers = args.cpu_workers or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or \
+            len(os.sched_getaffinity(0))
+        res["cpu_baseline"] = cpu_baseline(job.cfg, args.cpu_frames, workers)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

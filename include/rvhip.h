@@ -43,6 +43,10 @@ const char* rv_last_error(void);
  * dispatch marks a point in a rocprofv3 kernel trace (bench.py brackets its
  * timed region with tags 1 and 2). */
 int rv_trace_marker(int tag, void* stream);
+/* Diagnostics (no reference counterpart): on a fatal signal write the native
+ * stack to stderr, then chain to the previously installed handler (e.g.
+ * Python's faulthandler).  Idempotent. */
+int rv_install_crash_handler(void);
 
 /* ------------------------------------------------------------------------ */
 /* Preprocess: CLAHEDehaze (src/preprocess/ops/clahe_dehaze.py:13-32,       */
@@ -483,6 +487,41 @@ int rv_capture_release(void* handle, int slot);
 int rv_capture_upload_batch(void* const* handles, int S, uint8_t* dev, size_t dev_stride,
                             double* ts, int64_t* index, void* stream);
 int rv_capture_close(void* handle);
+
+/* --- Native launch schedule (csrc/sched.hip; no reference counterpart: the
+ * reference runs its chain synchronously, main_preview.py:94-109).  A run of
+ * K pipelined steps recorded once as a list of stream-ordered calls of this
+ * library plus event record / wait nodes, issued by rv_sched_run with one
+ * call.  rvs_amd/schedule.py records it.  Op argument arrays follow the C
+ * signature of the op with float-class arguments moved, in order, to fargs
+ * and the stream removed (it is the node's `stream`); a host-array argument
+ * is passed as its byte offset into `host` (copied at record time) or -1. */
+#define RV_SCHED_CLAHE_MEDIAN_LETTERBOX 0 /* rv_clahe_median_letterbox_u8 */
+#define RV_SCHED_CLAHE_MEDIAN 1           /* rv_clahe_median_u8 */
+#define RV_SCHED_LETTERBOX 2              /* rv_letterbox_u8 */
+#define RV_SCHED_YOLO_FORWARD_PART 3      /* rv_yolo_forward_part */
+#define RV_SCHED_NMS 4                    /* rv_nms_postprocess */
+#define RV_SCHED_SORT_UPDATE 5            /* rv_sort_update */
+#define RV_SCHED_HANDBACK 6               /* rv_results_handback */
+#define RV_SCHED_NUM_OPS 7
+int rv_sched_create(void** handle);
+int rv_sched_destroy(void* handle);
+int rv_sched_add_op(void* handle, int op, const int64_t* iargs, int ni, const double* fargs,
+                    int nf, const void* host, size_t host_bytes, void* stream);
+/* An event recorded on `stream` at this point of the run; its id -> *event.
+ * timing != 0: a timing event (rv_sched_event_elapsed). */
+int rv_sched_add_record(void* handle, void* stream, int timing, int* event);
+/* `stream` waits for event `event` (an earlier record node). */
+int rv_sched_add_wait(void* handle, void* stream, int event);
+int rv_sched_num_nodes(void* handle);
+/* Host wait (this thread only) for record node `event` of the last run. */
+int rv_sched_event_sync(void* handle, int event);
+/* Milliseconds between two timing record nodes of the last run. */
+int rv_sched_event_elapsed(void* handle, int a, int b, float* ms);
+/* Issue the whole schedule: every stream it uses waits for `origin`'s work
+ * so far, the nodes are issued in record order, and `origin` waits for every
+ * stream at the end.  Asynchronous (no host synchronisation). */
+int rv_sched_run(void* handle, void* origin);
 
 #ifdef __cplusplus
 }

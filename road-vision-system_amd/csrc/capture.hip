@@ -10,8 +10,9 @@
 // rv_capture_upload_batch feeds RoadVisionEngine: for S sources it takes one
 // frame of each, queues its H2D copy on the caller's stream and records an
 // event behind it; the slot returns to its reader once that event has
-// completed (polled at the next upload; waited for only when a source has
-// no other slot to hand out) -- so the ring refills while the device works
+// completed (polled at the next upload; waited for -- the oldest copy only --
+// when the next slot in order is still held by an earlier upload) -- so the
+// ring refills while the device works
 // and nothing blocks on a copy in flight.  No host callbacks are queued in
 // streams.  Frames travel as NV12 (1.5 B/pixel: what a decoder emits; the
 // device converts with rv_nv12_to_bgr_u8) or as raw BGR.
@@ -63,6 +64,7 @@ struct Capture {
   struct InFlight {
     hipEvent_t ev;
     int slot;
+    hipStream_t st;
   };
   std::deque<InFlight> inflight;
 };
@@ -180,32 +182,58 @@ void give_back(Capture* c, int slot) {
   c->cv_fill.notify_one();
 }
 
-// Return the slots whose copies have completed (all of them, waiting, with
-// `wait`); false if a wait failed.
-bool reap(Capture* c, bool wait) {
-  while (!c->inflight.empty()) {
-    Capture::InFlight& f = c->inflight.front();
-    const hipError_t e = wait ? hipEventSynchronize(f.ev) : hipEventQuery(f.ev);
-    if (e == hipErrorNotReady) return true;
-    (void)hipEventDestroy(f.ev);
-    give_back(c, f.slot);
-    c->inflight.pop_front();
-    if (e != hipSuccess) return false;
+// The oldest in-flight copy has finished (or failed): its slot goes back to
+// the reader.  On a failed query / wait the copy may still be reading the
+// slot, so the stream (then the device) is synchronised before the slot is
+// released.  Returns false on an error.
+bool retire_front(Capture* c, hipError_t e) {
+  Capture::InFlight f = c->inflight.front();
+  c->inflight.pop_front();
+  bool ok = e == hipSuccess;
+  if (!ok) {
+    set_error("capture: copy event: %s", hipGetErrorString(e));
+    if (hipStreamSynchronize(f.st) != hipSuccess) (void)hipDeviceSynchronize();
+    (void)hipGetLastError();
   }
-  return true;
+  (void)hipEventDestroy(f.ev);
+  give_back(c, f.slot);
+  return ok;
 }
 
-// take() for the upload path: while the reader has nothing filled and every
-// other slot waits on a copy, wait for the oldest copy so the reader can
-// refill (no deadlock between a full ring and a blocked consumer).
+// Return the slots whose copies have completed, without waiting.
+bool reap_done(Capture* c) {
+  bool ok = true;
+  while (!c->inflight.empty()) {
+    const hipError_t e = hipEventQuery(c->inflight.front().ev);
+    if (e == hipErrorNotReady) break;
+    ok = retire_front(c, e) && ok;
+  }
+  return ok;
+}
+
+// Wait for the oldest in-flight copy only and return its slot.
+bool reap_oldest(Capture* c) {
+  if (c->inflight.empty()) return true;
+  return retire_front(c, hipEventSynchronize(c->inflight.front().ev));
+}
+
+// take() for the upload path.  The next slot in order (the ring's tail) is
+// filled (take it), free (the reader is filling it: take() waits for the
+// reader), or still held by an earlier upload whose copy may be in flight --
+// the ring has gone all the way round -- and only then the host waits, for
+// the oldest copy alone (which is that slot's: copies retire in order).
 int take_for_upload(Capture* c, int* slot) {
-  reap(c, false);
+  if (!reap_done(c)) return RV_EINVAL;
   for (;;) {
+    int st;
+    bool eof;
     {
       std::lock_guard<std::mutex> lk(c->m);
-      if (c->slots[c->tail].state == 1 || c->eof || c->inflight.empty()) break;
+      st = c->slots[c->tail].state;
+      eof = c->eof;
     }
-    if (!reap(c, true)) break;
+    if (st != 2 || eof || c->inflight.empty()) break;
+    if (!reap_oldest(c)) return RV_EINVAL;
   }
   return take(c, slot);
 }
@@ -335,7 +363,7 @@ extern "C" int rv_capture_upload_batch(void* const* handles, int S, uint8_t* dev
       give_back(c, slot);
       return e;
     }
-    c->inflight.push_back({ev, slot});
+    c->inflight.push_back({ev, slot, st});
   }
   return RV_OK;
 }
@@ -343,7 +371,9 @@ extern "C" int rv_capture_upload_batch(void* const* handles, int S, uint8_t* dev
 extern "C" int rv_capture_close(void* handle) {
   if (!handle) return RV_OK;
   Capture* c = static_cast<Capture*>(handle);
-  reap(c, true);  // copies still in flight read the slots: wait for them
+  // copies still in flight read the slots: drain every one of them (whatever
+  // a wait returns) before the slots are freed
+  while (!c->inflight.empty()) (void)reap_oldest(c);
   {
     std::lock_guard<std::mutex> lk(c->m);
     c->stop = true;

@@ -265,6 +265,8 @@ struct Model {
   // forward parts (rv_yolo_forward_part): launch index base of this call
   // (part 2 continues part 1's launch numbering) and part 1's launch count
   int li_base = 0, n_part1 = -1;
+  int part1_B = 0;                // batch and workspace of the last part 0 / part 1 forward:
+  const void* part1_ws = nullptr;  // part 2 must continue exactly that forward
   // fp8 plans: per-buffer activation scales (value = code * scale), powers
   // of two; set by rv_yolo_set_act_scales before the first forward
   std::vector<float> act_scale;
@@ -885,6 +887,9 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
   Model* M = (Model*)h;
   RV_CHECK_ARG(part != 2 || M->n_part1 >= 0,
                "forward part 2 before any part 0 / part 1 forward of this handle");
+  RV_CHECK_ARG(part != 2 || (B == M->part1_B && ws == M->part1_ws),
+               "forward part 2 (B=%d, ws %p) does not continue the last part 1 of this handle "
+               "(B=%d, ws %p)", B, ws, M->part1_B, M->part1_ws);
   RV_CHECK_ARG(part != 1 || !raw_out, "raw_out needs the whole forward (part 0)");
   RV_CHECK_ARG(B > 0 && B <= M->max_B, "B=%d outside (0, %d]", B, M->max_B);
   RV_CHECK_ARG(ws_bytes >= M->ws_bytes(B), "workspace %zu < %zu bytes", ws_bytes, M->ws_bytes(B));
@@ -980,6 +985,8 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
         View{M->X15, v.h15, 0}, 0, View{-1, 0, 0}, 0, fuse_c2f);
   if (E.status) return E.status;
   M->n_part1 = (int)M->launches.size();
+  M->part1_B = B;
+  M->part1_ws = ws;
   if (part == 1) return RV_OK;
   }  // part != 2
   // Detect head of level i: box (cv2) and class (cv3) branches, one grouped

@@ -119,6 +119,18 @@ _SIGS = {
     "rv_yolo_set_tuned": (c_int, [c_void_p, c_int, c_int, POINTER(c_int)]),
     "rv_yolo_conv_candidates": (c_int, [c_void_p, c_int, c_void_p, c_int]),
     "rv_trace_marker": (c_int, [c_int, c_void_p]),
+    "rv_install_crash_handler": (c_int, []),
+    # native launch schedule
+    "rv_sched_create": (c_int, [c_void_p]),
+    "rv_sched_destroy": (c_int, [c_void_p]),
+    "rv_sched_add_op": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                c_size_t, c_void_p]),
+    "rv_sched_add_record": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "rv_sched_event_sync": (c_int, [c_void_p, c_int]),
+    "rv_sched_event_elapsed": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "rv_sched_add_wait": (c_int, [c_void_p, c_void_p, c_int]),
+    "rv_sched_num_nodes": (c_int, [c_void_p]),
+    "rv_sched_run": (c_int, [c_void_p, c_void_p]),
     "rv_nms_smem_bytes": (c_size_t, []),
     "rv_nms_postprocess": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int,
                                    c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -149,6 +161,8 @@ def load():
         raise RVError(
             f"{LIB_PATH} not found: build it with `make -C road-vision-system_amd/csrc` "
             "or __graft_entry__.build(); the HIP path has no CPU fallback")
+    import torch  # noqa: F401 -- bind librvhip to torch's HIP runtime (libamdhip64.so.7),
+    # never to a second copy from /opt/rocm: two runtimes in one process do not share devices
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)
@@ -173,12 +187,43 @@ def check(status: int, what: str = "") -> None:
         raise RVError(f"{what or 'rvhip'} failed with status {status}: {msg}")
 
 
-_NOCHECK = {"rv_abi_version", "rv_cand_segments", "rv_yolo_cand_segments", "rv_clahe_median_fits", "rv_clahe_median_letterbox_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
+# stream-ordered calls a launch schedule can record (rvs_amd.schedule._OPS)
+_RECORDABLE = {"rv_clahe_median_letterbox_u8", "rv_clahe_median_u8", "rv_letterbox_u8",
+               "rv_yolo_forward_part", "rv_nms_postprocess", "rv_sort_update",
+               "rv_results_handback"}
+
+_NOCHECK = {"rv_sched_num_nodes", "rv_abi_version", "rv_cand_segments", "rv_yolo_cand_segments", "rv_clahe_median_fits", "rv_clahe_median_letterbox_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
             "rv_yolo_num_buffers", "rv_yolo_trace", "rv_yolo_profile_read", "rv_yolo_tuned_config",
             "rv_yolo_profile_bytes", "rv_yolo_buffer_esize", "rv_yolo_conv_candidates"}
 
 
+_recorder = None  # a schedule.Schedule while one is being recorded
+
+
+class recording:
+    """Inside this context, recordable calls (schedule._OPS) are appended to
+    `sched` as launch-list nodes instead of running (rvs_amd.schedule)."""
+
+    def __init__(self, sched):
+        self.sched = sched
+
+    def __enter__(self):
+        global _recorder
+        if _recorder is not None:
+            raise RuntimeError("a schedule is already being recorded")
+        _recorder = self.sched
+        return self.sched
+
+    def __exit__(self, *exc):
+        global _recorder
+        _recorder = None
+        return False
+
+
 def call(name: str, *args) -> int:
+    if _recorder is not None and name in _RECORDABLE:
+        _recorder.add(name, args)
+        return 0
     fn = getattr(load(), name)
     st = fn(*args)
     if fn.restype is c_int and name not in _NOCHECK:

@@ -10,7 +10,6 @@ record and materialises the reference's ``List[Detection]`` per stream.
 """
 from __future__ import annotations
 
-import math
 from typing import List, Sequence
 
 import numpy as np
@@ -40,6 +39,7 @@ class Record:
         self.S, self.dmax = int(S), int(dmax)
         self.nbytes = record_bytes(self.S, self.dmax)
         self.host = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True) if host else None
+        self.seq = 0  # hand-backs issued into this record (RoadVisionEngine.results checks it)
 
     def arrays(self):
         """(counts (S,), rows (S, dmax) structured) views of the host record.
@@ -63,15 +63,39 @@ def handback(dets: torch.Tensor, det_n: torch.Tensor, track_id, distance_m, spee
 
 def to_detections(n: np.ndarray, rows: np.ndarray, names: Sequence[str]) -> List[List[Detection]]:
     """The reference's Detection lists (yolo_ultralytics.py:48-52 fields plus
-    the tracker's track_id / distance_m / speed_kmh; NaN / -1 -> None)."""
-    out = []
+    the tracker's track_id / distance_m / speed_kmh; NaN / -1 -> None).
+
+    Column-wise: every field of all valid rows is converted to Python
+    objects in one numpy pass, then each Detection is created without its
+    generated __init__ (the dataclass keeps its fields in __dict__, so the
+    objects are equal to -- and behave exactly like -- Detection(...) ones);
+    ~3x faster than building them row by row, so a host consumer keeps up
+    with the device (bench.py's timed region builds them)."""
+    S, dmax = rows.shape
+    cnt = np.clip(np.asarray(n[:S], np.int64), 0, dmax)
+    r = rows[np.arange(dmax)[None, :] < cnt[:, None]]
     nn = len(names)
-    for s in range(rows.shape[0]):
-        lst = []
-        for x1, y1, x2, y2, conf, k, tid, _, dist, spd in rows[s, :int(n[s])].tolist():
-            lst.append(Detection(x1, y1, x2, y2, conf, k, str(names[k]) if 0 <= k < nn else str(k),
-                                 None if tid < 0 else tid,
-                                 None if math.isnan(dist) else dist,
-                                 None if math.isnan(spd) else spd))
-        out.append(lst)
+    kl = r["cls"].tolist()
+    cname = [str(names[k]) if 0 <= k < nn else str(k) for k in kl]
+    t = r["track_id"]
+    tid = np.where(t < 0, None, t.astype(object)).tolist()
+    d = r["dist"]
+    dist = np.where(np.isnan(d), None, d.astype(object)).tolist()
+    sp = r["speed"]
+    spd = np.where(np.isnan(sp), None, sp.astype(object)).tolist()
+    new = object.__new__
+    flat = []
+    app = flat.append
+    for x1, y1, x2, y2, c, k, nm, ti, di, si in zip(r["x1"].tolist(), r["y1"].tolist(),
+                                                    r["x2"].tolist(), r["y2"].tolist(),
+                                                    r["conf"].tolist(), kl, cname, tid, dist, spd):
+        o = new(Detection)
+        o.__dict__ = {"x1": x1, "y1": y1, "x2": x2, "y2": y2, "conf": c, "cls_id": k,
+                      "cls_name": nm, "track_id": ti, "distance_m": di, "speed_kmh": si}
+        app(o)
+    out = []
+    i = 0
+    for c in cnt.tolist():
+        out.append(flat[i:i + c])
+        i += c
     return out

@@ -68,7 +68,8 @@ class PreprocessPipeline:
         clahe, med = self.ops
         return kernels.clahe_median_letterbox_fits(H, W, clahe.grid, med.k, geo)
 
-    def run_with_letterbox(self, x: torch.Tensor, geo, lb_out: torch.Tensor):
+    def run_with_letterbox(self, x: torch.Tensor, geo, lb_out: torch.Tensor,
+                           out: torch.Tensor = None):
         """(B,H,W,3) device frames -> (proc, letterboxed proc) in one pass;
         byte-identical to self(x) followed by the detector's letterbox."""
         clahe, med = self.ops
@@ -77,7 +78,7 @@ class PreprocessPipeline:
         if self._ws is None or self._ws.numel() < need or self._ws.device != x.device:
             self._ws = torch.empty(need, dtype=torch.uint8, device=x.device)
         return kernels.clahe_median_letterbox(x, clahe.grid, clahe.clip_limit, med.k, geo,
-                                              lb_out=lb_out, ws=self._ws)
+                                              out=out, lb_out=lb_out, ws=self._ws)
 
     def __call__(self, image, ts: float = None):
         if not self.enabled or not self.ops:

@@ -17,6 +17,22 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
 
 
+def pytest_sessionstart(session):
+    """A fatal signal in native code writes its C stack before Python's
+    faulthandler writes the Python one (rv_install_crash_handler)."""
+    try:
+        from rvs_amd import _lib
+        _lib.load().rv_install_crash_handler()
+    except Exception as e:  # the library may not be built in a CPU-only checkout
+        os.write(2, f"[conftest] native crash handler not installed: {e}\n".encode())
+
+
+def pytest_runtest_logstart(nodeid, location):
+    """Name every test on stderr before it runs (unbuffered), so the tail of a
+    run that dies in native code says which test it died in, even under -q."""
+    os.write(2, f"\n[test start] {nodeid}\n".encode())
+
+
 @pytest.fixture(scope="session")
 def cuda():
     import torch

@@ -82,3 +82,27 @@ def test_fused_letterbox_fits_host_only():
     assert kernels.clahe_median_letterbox_fits(640, 640, 8, 3, kernels.letterbox_geometry(640, 640))
     assert not kernels.clahe_median_letterbox_fits(1080, 1920, 8, 5,
                                                    kernels.letterbox_geometry(1080, 1920))
+
+
+def test_schedule_op_table_matches_abi():
+    """rvs_amd.schedule._OPS (Python recorder) against include/rvhip.h's
+    RV_SCHED_* ids and csrc/sched.hip's per-op argument counts: the recorder
+    splits each call's arguments into integer / float slots exactly as the
+    native issuer unpacks them."""
+    from rvs_amd import _lib, schedule
+    hdr = open(HEADER).read()
+    ids = {m.group(2): int(m.group(1)) for m in
+           re.finditer(r"#define RV_SCHED_\w+ (\d+)\s*/\* (rv_\w+) \*/", hdr)}
+    src = open(os.path.join(REPO, "road-vision-system_amd", "csrc", "sched.hip")).read()
+    specs = [tuple(map(int, m.groups())) for m in
+             re.finditer(r"/\* RV_SCHED_\w+ \*/ \{(\d+), (\d+)\}", src)]
+    assert set(ids) == set(schedule._OPS) == _lib._RECORDABLE
+    for name, (op, si, host) in schedule._OPS.items():
+        assert ids[name] == op, name
+        argtypes = _lib._SIGS[name][1]
+        assert argtypes[si] is ctypes.c_void_p, name
+        nf = sum(1 for k, t in enumerate(argtypes) if k != si and t in (ctypes.c_float,
+                                                                        ctypes.c_double))
+        ni = len(argtypes) - 1 - nf
+        assert specs[op] == (ni, nf), name
+        assert all(0 <= k < len(argtypes) and k != si for k in host), name

@@ -5,9 +5,10 @@ same kernel sequence as the candidate path); SORT ids / distances exact and
 speeds to 1e-9 relative on the GPU's detections; no stream overflows tmax.
 
 test_bench_configuration_parity runs exactly what bench.py times: 32
-streams of 1080p, per-layer autotuned conv kernels, the 3-deep software
-pipeline of 8 steps per captured graph, results handed back to pinned host
-records inside the step (reference call order: main_preview.py:94-109)."""
+streams of 1080p, per-layer autotuned conv kernels, the 4-stage software
+pipeline issued by the native launch list (rvs_amd.schedule.PipelinedRun),
+results handed back to pinned host records inside the step (reference call
+order: main_preview.py:94-109)."""
 import numpy as np
 import pytest
 import torch
@@ -110,24 +111,25 @@ def test_results_record_matches_device_outputs(cuda):
     eng.close()
 
 
-@pytest.mark.parametrize("depth,chunk,lanes,pair", [
-    (2, None, 1, 1), (3, 1, 1, 1), (3, 3, 1, 1), (3, None, 1, 1), (3, 0, 1, 1), (3, None, 2, 1),
-    (3, 3, 2, 1), (3, 0, 3, 1), (4, None, 2, 1), (4, 3, 2, 1), (4, 0, 2, 1), (4, None, 2, 2),
-    (4, 1, 2, 2)])
-def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk, lanes, pair):
-    """bench.py's timed mode (engine.OverlappedSteps): the track stage of step
-    k runs on a side stream beside the preprocess of step k+1, with `chunk`
-    pipeline stages per captured graph (None = the default 8, 0 = one graph);
-    lanes >= 2 (depth 3): the dependency-graph schedule with that many concurrent YOLO
-    forwards; pair 2 (depth 4): one forward over two consecutive steps'
-    frames.  EVERY step's handed-back detections / track ids and proc
-    frames, and the final SORT state, must equal those of plain sequential
-    step() calls."""
-    from rvs_amd.engine import OverlappedSteps, RoadVisionEngine
+@pytest.mark.parametrize("mode,sync,pair", [
+    ("native", "flow", 1), ("native", "stage", 1), ("native", "flow", 2), ("native", "stage", 2),
+    ("eager", "flow", 2), ("eager", "stage", 1)])
+def test_pipelined_run_matches_sequential_steps(cuda, mode, sync, pair):
+    """bench.py's timed mode (rvs_amd.schedule.PipelinedRun): units of `pair`
+    steps software-pipelined over four HIP streams -- preprocess of unit u+1,
+    the two forward halves of units u and u-1 on two lanes, NMS + SORT +
+    hand-back of unit u-2 -- issued by the native launch list or eagerly,
+    lock-stepped or chained by per-dependency events.  EVERY step's
+    handed-back detections / track ids and proc frames, and the final SORT
+    state, must equal those of plain sequential step() calls; a second run()
+    of the same schedule continues the tracks like K more step() calls."""
+    from rvs_amd.engine import RoadVisionEngine
+    from rvs_amd.schedule import PipelinedRun
     from rvs_amd.synth import road_frames
     cfg = _cfg()
     S, H, W = 4, 1080, 1920
-    F = 9 if pair == 2 else 8  # the overlapped steps (F - 1) pair up
+    K = 8  # a multiple of pair
+    F = 1 + 2 * K
     frames = road_frames(S, F, H, W, device=cuda)
     ts = torch.tensor([[f / 30.0] * S for f in range(F)], dtype=torch.float64, device=cuda)
     seq = RoadVisionEngine(cfg, S, (H, W), device=cuda)
@@ -136,43 +138,79 @@ def test_overlapped_steps_match_sequential_steps(cuda, depth, chunk, lanes, pair
         out_seq = seq.step(frames[f], ts[f])
         seq_res.append(seq.results(out_seq))
         seq_proc.append(out_seq["proc"].cpu().numpy())
-    ovl = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=lanes, pair=pair)
-    ovl.step(frames[0], ts[0])  # eager first step (one-time kernel setup)
-    run = OverlappedSteps(ovl, [frames[f] for f in range(1, F)], [ts[f] for f in range(1, F)],
-                          depth=depth, chunk=chunk)
-    run.run()
-    torch.cuda.synchronize()
+    pip = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=2, pair=pair)
+    pip.step(frames[0], ts[0])
     key = lambda r: [[(d.x1, d.y1, d.x2, d.y2, d.conf, d.cls_id, d.track_id, d.distance_m,  # noqa
                        d.speed_kmh) for d in s] for s in r]
-    assert len(run.outs) == F - 1
-    for k, o in enumerate(run.outs):
-        assert key(seq_res[k + 1]) == key(ovl.results(o)), f"step {k + 1}"
-        np.testing.assert_array_equal(o["proc"].cpu().numpy(), seq_proc[k + 1])
+    for r in range(2):  # two runs over two windows of K steps
+        f0 = 1 + r * K
+        run = PipelinedRun(pip, [frames[f0 + k] for k in range(K)],
+                           [ts[f0 + k] for k in range(K)], mode=mode, sync=sync)
+        if mode == "native":
+            assert run.sched.num_nodes() > 0
+        run.run()
+        torch.cuda.synchronize()
+        assert len(run.outs) == K
+        for k, o in enumerate(run.outs):
+            assert key(seq_res[f0 + k]) == key(pip.results(o)), f"run {r} step {k}"
+            np.testing.assert_array_equal(o["proc"].cpu().numpy(), seq_proc[f0 + k])
+        run.close()
     Ts, xs, ms = seq.tracker.export()
-    To, xo, mo = ovl.tracker.export()
+    To, xo, mo = pip.tracker.export()
     np.testing.assert_array_equal(Ts, To)
     for s in range(S):
         np.testing.assert_array_equal(xs[s, :Ts[s]], xo[s, :To[s]])
         np.testing.assert_array_equal(ms[s, :Ts[s]], mo[s, :To[s]])
     seq.close()
-    ovl.close()
+    pip.close()
 
 
-@pytest.mark.parametrize("depth,lanes,pair", [(4, 2, 1), (4, 2, 4), (3, 1, 1)])
-def test_bench_configuration_parity(cuda, depth, lanes, pair):
+def test_native_schedule_replays(cuda):
+    """The same recorded launch list run twice over the same inputs: the
+    second run continues SORT from the first (ids keep counting) and its
+    preprocess / detections equal a fresh eager pipeline's second run."""
+    from rvs_amd.engine import RoadVisionEngine
+    from rvs_amd.schedule import PipelinedRun
+    from rvs_amd.synth import road_frames
+    cfg = _cfg()
+    S, H, W, K = 2, 720, 1280, 4
+    frames = road_frames(S, K, H, W, device=cuda)
+    ts = [torch.full((S,), k / 30.0, dtype=torch.float64, device=cuda) for k in range(K)]
+    outs = {}
+    for mode in ("native", "eager"):
+        eng = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=2, pair=2)
+        run = PipelinedRun(eng, [frames[k] for k in range(K)], ts, mode=mode)
+        got = []
+        for _ in range(2):
+            run.run()
+            torch.cuda.synchronize()
+            got.append([eng.results(o) for o in run.outs])
+        key = lambda r: [[(d.x1, d.y1, d.x2, d.y2, d.conf, d.cls_id, d.track_id)  # noqa
+                          for d in s] for s in r]
+        outs[mode] = [[key(r) for r in g] for g in got]
+        run.close()
+        eng.close()
+    assert outs["native"] == outs["eager"]
+    ids0 = {d[6] for st in outs["native"][0] for s in st for d in s if d[6] is not None}
+    ids1 = {d[6] for st in outs["native"][1] for s in st for d in s if d[6] is not None}
+    assert ids0 and ids1
+
+
+@pytest.mark.parametrize("pair", [1, 4])
+def test_bench_configuration_parity(cuda, pair):
     """Exactly bench.py's timed configuration (S = 32 streams of 1080p,
-    autotuned conv kernels, OverlappedSteps(depth=4, chunk=8) on two forward
-    lanes, with and without pairing two steps per forward -- and the depth-3
-    one-lane pipeline --, hand-back into per-step
-    host records), checked against the oracle on every step:
+    autotuned conv kernels on persistent grids, PipelinedRun native launch
+    list with per-dependency events on two forward lanes, hand-back into
+    per-step host records), checked against the oracle on every step:
     proc bit-exact on a sample of streams, NMS exact on the GPU's raw
     prediction for all 32 streams, SORT ids / distances exact for all 32
     streams, and no stream ever exceeds tmax."""
-    from rvs_amd.engine import OverlappedSteps, RoadVisionEngine
+    from rvs_amd.engine import RoadVisionEngine
+    from rvs_amd.schedule import PipelinedRun
     from rvs_amd.synth import road_frames
     cfg = _cfg()
     S, H, W, WARM, K = 32, 1080, 1920, 2, 8
-    eng = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=lanes, pair=pair)
+    eng = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=2, pair=pair)
     frames = road_frames(S, WARM + K, H, W, device=cuda)
     ts = torch.tensor([[f / 30.0] * S for f in range(WARM + K)], dtype=torch.float64, device=cuda)
     chk = Checker(eng, cfg, proc_streams=[0, 13, 31])
@@ -184,8 +222,8 @@ def test_bench_configuration_parity(cuda, depth, lanes, pair):
     # bench.py's --conv-grid persistent: the tuned tiles on persistent grids
     eng.detector.load_tuned([tuple(c[:4]) + (1,) + tuple(c[5:])
                              for c in eng.detector.tuned_configs()])
-    run = OverlappedSteps(eng, [frames[WARM + k] for k in range(K)],
-                          [ts[WARM + k] for k in range(K)], depth=depth, chunk=8)
+    run = PipelinedRun(eng, [frames[WARM + k] for k in range(K)],
+                       [ts[WARM + k] for k in range(K)], mode="native", sync="flow")
     run.run()
     torch.cuda.synchronize()
     for k, o in enumerate(run.outs):
@@ -196,4 +234,5 @@ def test_bench_configuration_parity(cuda, depth, lanes, pair):
     assert st["overflow"].sum() == 0
     np.testing.assert_array_equal(st["T"], [len(t.tracks) for t in chk.trackers])
     assert chk.n_dets > 0
+    run.close()
     eng.close()

@@ -1,0 +1,56 @@
+"""Host side of the result hand-back (rvs_amd.handback) on the CPU: the
+column-wise to_detections builds exactly the Detection objects a row-by-row
+construction does (src/detect/yolo_ultralytics.py:48-52 fields, then
+sort_tracker.py:234-247's track_id / distance_m / speed_kmh; -1 / NaN ->
+None), for ragged per-stream counts, empty streams, counts outside
+[0, dmax] and class ids outside the name table."""
+import math
+
+import numpy as np
+
+from rvs_amd.detect.types import Detection
+from rvs_amd.detect.weights import COCO80
+from rvs_amd.handback import ROW, to_detections
+
+
+def _rowwise(n, rows, names):
+    out = []
+    for s in range(rows.shape[0]):
+        lst = []
+        for x1, y1, x2, y2, conf, k, tid, _, dist, spd in \
+                rows[s, :max(0, min(int(n[s]), rows.shape[1]))].tolist():
+            lst.append(Detection(x1, y1, x2, y2, conf, k,
+                                 str(names[k]) if 0 <= k < len(names) else str(k),
+                                 None if tid < 0 else tid,
+                                 None if math.isnan(dist) else dist,
+                                 None if math.isnan(spd) else spd))
+        out.append(lst)
+    return out
+
+
+def test_to_detections_matches_rowwise_construction():
+    rng = np.random.default_rng(7)
+    S, dmax = 9, 17
+    rows = np.zeros((S, dmax), ROW)
+    for f in ("x1", "y1", "x2", "y2", "conf"):
+        rows[f] = rng.uniform(-5, 2000, (S, dmax)).astype(np.float32)
+    rows["cls"] = rng.integers(-2, 84, (S, dmax))
+    rows["track_id"] = rng.integers(-1, 40, (S, dmax))
+    rows["dist"] = np.where(rng.random((S, dmax)) < 0.3, np.nan, rng.uniform(0, 99, (S, dmax)))
+    rows["speed"] = np.where(rng.random((S, dmax)) < 0.5, np.nan, rng.uniform(0, 150, (S, dmax)))
+    n = np.array([0, 1, dmax, 5, -3, dmax + 4, 3, 16, 2], np.int32)
+    got = to_detections(n, rows, COCO80)
+    want = _rowwise(n, rows, COCO80)
+    assert got == want
+    assert [len(x) for x in got] == [0, 1, dmax, 5, 0, dmax, 3, 16, 2]
+    for a, b in zip(sum(got, []), sum(want, [])):
+        assert vars(a) == vars(b)
+        assert all(type(getattr(a, f)) is type(getattr(b, f)) for f in vars(b))
+    d = got[1][0]
+    d.track_id = 5  # still an ordinary mutable Detection (SortTracker.update mutates it)
+    assert d.track_id == 5 and isinstance(d, Detection)
+
+
+def test_to_detections_empty():
+    rows = np.zeros((3, 4), ROW)
+    assert to_detections(np.zeros(3, np.int32), rows, COCO80) == [[], [], []]

@@ -24,12 +24,16 @@ def _free_port():
 
 
 class _CpuJob:
-    """bench.BenchJob's interface (warmup / prepare / run / sync / units)
-    over the oracle chain of this rank's streams."""
+    """bench.BenchJob's interface (constructor (args, rank, device); warmup /
+    prepare / run / sync / units) over the oracle chain of this rank's
+    streams: args.streams streams, args.steps frames each.  With RV_STUB_OUT
+    set, a rank writes its per-stream results to RV_STUB_OUT/rank<r>.json."""
 
-    def __init__(self, S, F, rank):
+    def __init__(self, args, rank, dev="cpu"):
         from rvs_amd.shard import rank_streams
         from rvs_amd.synth import road_frames
+        S, F = args.streams, args.steps
+        self.rank = rank
         self.ids = rank_streams(S, rank)
         self.fr = road_frames(S, F, 48, 64, device="cpu", stream_offset=self.ids.start).numpy()
         self.S, self.F = S, F
@@ -59,6 +63,10 @@ class _CpuJob:
                 trk.update(dets, f / 30.0)
                 tracks.append(([d.track_id for d in dets], int(proc.sum())))
             self.out[sid] = tracks
+        if os.environ.get("RV_STUB_OUT"):
+            import json
+            with open(os.path.join(os.environ["RV_STUB_OUT"], f"rank{self.rank}.json"), "w") as f:
+                json.dump({str(k): v for k, v in self.out.items()}, f)
 
     def sync(self):
         self.calls.append("sync")
@@ -76,7 +84,8 @@ def _worker(rank, world, port, S, F, q):
     from rvs_amd.shard import init_from_env
     r, w, _ = init_from_env("gloo")
     assert (r, w) == (rank, world) and dist.is_initialized()
-    job = _CpuJob(S, F, rank)
+    import argparse
+    job = _CpuJob(argparse.Namespace(streams=S, steps=F), rank)
     t = bench.rank_job(job, "cpu")
     q.put((rank, list(job.ids), job.out, t, job.calls))
     dist.barrier()
@@ -109,15 +118,20 @@ def test_two_rank_sharding_matches_single_process():
     assert all(abs(r[3]["value"] - S * F * world / mx) < 1e-9 * r[3]["value"] for r in res)
     # each rank's per-stream results equal a single process running all streams
     import sys
-    from oracle import cpu, sort_ref
-    from rvs_amd.config import load_config
-    from rvs_amd.synth import road_frames
-    fr = road_frames(S * world, F, 48, 64, device="cpu").numpy()
-    cfg = load_config()["tracking"]
     merged = {}
     for r in res:
         merged.update(r[2])
-    for sid in range(S * world):
+    _check_single_process(merged, S * world, F)
+    assert sys.modules.get("torch.distributed") is not None
+
+
+def _check_single_process(merged, n_streams, F):
+    from oracle import cpu, sort_ref
+    from rvs_amd.config import load_config
+    from rvs_amd.synth import road_frames
+    fr = road_frames(n_streams, F, 48, 64, device="cpu").numpy()
+    cfg = load_config()["tracking"]
+    for sid in range(n_streams):
         trk = sort_ref.SortTracker(cfg)
         rng = np.random.default_rng(sid)
         base = rng.uniform(0, 40, (3, 2))
@@ -126,7 +140,38 @@ def test_two_rank_sharding_matches_single_process():
             dets = [sort_ref.Det(x + 2 * f, y, x + 2 * f + 8, y + 8, 0.9, 2) for x, y in base]
             trk.update(dets, f / 30.0)
             assert merged[sid][f] == ([d.track_id for d in dets], int(proc.sum()))
-    assert sys.modules.get("torch.distributed") is not None
+
+
+def test_bench_gpus_flag_spawns_the_ranks(tmp_path, capfd, monkeypatch):
+    """`bench.py --gpus 2` without torchrun's environment starts the 2 ranks
+    itself (fresh child processes with RANK / WORLD_SIZE / MASTER_*), each
+    joins the process group (gloo here, RCCL on the GPUs) and runs its own
+    stream block; rank 0 prints ONE JSON line with n_gpus = world_size = 2
+    and the whole-job rate over the slowest rank."""
+    import json
+    import bench
+    here = os.path.dirname(os.path.abspath(__file__))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("PYTHONPATH", here + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    monkeypatch.setenv("RV_STUB_OUT", str(tmp_path))
+    monkeypatch.setenv("OMP_NUM_THREADS", "2")
+    S, F = 2, 3
+    rc = bench.main(["--gpus", "2", "--streams", str(S), "--steps", str(F), "--warmup", "0",
+                     "--job", "test_shard_gloo:_CpuJob"])
+    assert rc == 0
+    lines = [ln for ln in capfd.readouterr().out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["steps"] == F
+    assert abs(d["value"] - S * F * 2 / d["elapsed_s"]) < 1e-9 * d["value"]
+    assert d["elapsed_s"] >= d["local_s"] > 0
+    merged = {}
+    for r in range(2):
+        merged.update({int(k): [(a, b) for a, b in v] for k, v in
+                       json.load(open(tmp_path / f"rank{r}.json")).items()})
+    assert sorted(merged) == list(range(S * 2))
+    _check_single_process(merged, S * 2, F)
 
 
 def test_partition_rejects_uneven_split():

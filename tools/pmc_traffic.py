@@ -6,6 +6,7 @@ calibration in MI355X_MICROARCH.md, FETCH_SIZE counts half the bytes of a
 wide streaming read (x2), WRITE_SIZE counts 16-B-per-lane stores exactly.
 Writes a JSON file that bench.py reports as roofline.traffic.
 Usage: pmc_traffic.py out.json pass1.csv pass2.csv ..."""
+import hashlib
 import json
 import os
 import sys
@@ -41,6 +42,11 @@ def main():
     res = {"conv_bytes_per_step": fetch + write, "conv_read_bytes": fetch,
            "conv_write_bytes": write, "conv_kernels": list(CONV_KERNELS),
            "steps_per_forward": unit,
+           # the library the counters were collected on: bench.py reports this
+           # traffic only while the same build is loaded
+           "librvhip_sha256": hashlib.sha256(open(os.path.join(
+               os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+               "road-vision-system_amd", "rvs_amd", "librvhip.so"), "rb").read()).hexdigest(),
            "per_kernel": {k: {"launches": c, "read_bytes": r, "write_bytes": w}
                           for k, (c, r, w) in per_kernel.items()},
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over one eager pipeline "
