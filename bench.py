@@ -165,6 +165,7 @@ class BenchJob:
         self.cons = {}
         self.records = None
         self.device_end = 0.0
+        self.issue_s = 0.0
         torch.cuda.synchronize()
 
     def warmup(self):
@@ -224,6 +225,7 @@ class BenchJob:
         from rvs_amd import _lib
         st = _lib.stream_ptr()
         _lib.call("rv_trace_marker", 1, st)  # brackets the timed region in a kernel trace
+        t0 = time.perf_counter()
         if self.runner is not None:
             self.runner.run()
             wait = self.runner.wait_step
@@ -235,6 +237,7 @@ class BenchJob:
                 e.record()
                 evs.append(e)
             wait = lambda k: evs[k].synchronize()  # noqa: E731
+        self.issue_s = time.perf_counter() - t0
         _lib.call("rv_trace_marker", 2, st)
         if self.consume != "off":
             self._consumer = threading.Thread(target=self._consume,
@@ -314,6 +317,15 @@ def _conv_pass(job, mode: str, tags):
     torch.cuda.synchronize()
     lib.rv_yolo_profile(h, 0)
     valid = cv >= 0
+    table = os.environ.get("RV_CONV_TABLE")
+    if table:  # per-launch table of this pass (tools: per-layer roofline)
+        from rvs_amd.detect.weights import conv_list
+        names = [c[0] for c in conv_list(eng.variant)]
+        with open(f"{table}_{mode}.json", "w") as f:
+            json.dump({"mode": mode, "forwards": int(nf), "batch": eng.S * eng.pair,
+                       "launches": [{"conv": names[int(cv[i])], "us": ms[i] / max(nf, 1) * 1e3,
+                                     "gflop": fl[i] / 1e9, "mb": by[i] / 1e6}
+                                    for i in range(n) if cv[i] >= 0]}, f, indent=0)
     # every profiled forward covers `pair` steps -> per step
     per = eng.pair
     return (float(ms[valid].sum()) / max(nf, 1) / per, float(fl[valid].sum()) / per,
@@ -539,6 +551,7 @@ def main(argv=None):
                              "soon as the step's record is handed back"
                              if job.consume == "consume" else "off"),
                 "record_bytes_per_step": job.records[0].nbytes}
+    handback["host_issue_ms"] = round(job.issue_s * 1e3, 3)
     if job.consume == "consume" and cons:
         handback["detections_per_step"] = round(cons["detections"] / K, 1)
         handback["materialise_ms_per_step"] = round(cons["busy_s"] / K * 1e3, 3)

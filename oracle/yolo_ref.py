@@ -133,9 +133,15 @@ def fp8_scale(amax: float) -> float:
 
 
 def quant_fp8(t: torch.Tensor, scale: float) -> torch.Tensor:
-    """Stored value of t in an fp8 buffer of this scale: code(t / s) * s."""
-    q = e4m3_value(e4m3_code(t.detach().double().numpy() / scale)) * scale
-    return torch.from_numpy(q.astype(np.float32))
+    """Stored value of t in an fp8 buffer of this scale: code(t / s) * s.
+    t / s is exact in f32 (power-of-two s), and torch's f32 -> float8_e4m3fn
+    conversion rounds to nearest even like e4m3_code once the value is
+    saturated to +-448 (tests/test_fp8_cpu.py checks the two agree on every
+    code, every midpoint and the subnormal range); ~45x faster than the
+    table search, which keeps the fp8 oracle usable at 1280x1280."""
+    s = float(scale)
+    q = (t.detach().float() / s).clamp(-448.0, 448.0).to(torch.float8_e4m3fn)
+    return q.to(torch.float32) * s
 
 
 def quant_weight_fp8(w: np.ndarray):

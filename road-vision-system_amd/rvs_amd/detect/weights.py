@@ -69,20 +69,53 @@ def conv_list(variant: int) -> List[Tuple[str, int, int, int, int, int]]:
 _CALIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "synthetic_calib.npz")
 
 
+SMOOTH_KERNEL = "delta"  # spatial profile of the coherent part: "delta" (centre tap) or "blur"
+
+
+def base_weights(rng, seed: int, idx: int, cin: int, cout: int, k: int, smooth: float):
+    """Base (pre-calibration) weights and bias of conv `idx`: unit-fan-in
+    He-normal weights (drawn from `rng`, the same stream for every `smooth`),
+    mixed with weight `smooth` in [0, 1) of a channel-coherent part -- per
+    output channel a signed gain times one positive per-input-channel profile
+    on the centre tap (SMOOTH_KERNEL), rows scaled to the same norm as the
+    random part.  Trained conv filters are spatially smooth and
+    their inputs redundant, so noise added to an activation (quantisation,
+    accumulation order) is averaged down layer by layer; pure random weights
+    pass it on at full strength (the chaotic regime)."""
+    w = rng.normal(0, 1 / np.sqrt(cin * k * k), size=(cout, cin, k, k)).astype(np.float32)
+    b = rng.normal(0, 0.05, size=(cout,)).astype(np.float32)
+    if smooth > 0:
+        srng = np.random.default_rng([seed, 7919, idx])
+        g = np.zeros((k, k))
+        if SMOOTH_KERNEL == "blur" and k == 3:
+            g1 = np.array([1.0, 2.0, 1.0])
+            g = np.outer(g1, g1)
+        else:
+            g[k // 2, k // 2] = 1.0
+        u = srng.uniform(0.5, 1.5, cin)
+        a = srng.choice([-1.0, 1.0], cout) * srng.uniform(0.5, 1.5, cout)
+        st = a[:, None, None, None] * u[None, :, None, None] * g[None, None]
+        st /= np.sqrt((st ** 2).sum(axis=(1, 2, 3), keepdims=True))
+        w = (np.sqrt(1 - smooth) * w + np.sqrt(smooth) * st).astype(np.float32)
+    return w, b
+
+
 def synthetic_weights(variant: int, seed: int = 0) -> np.ndarray:
     """Seeded BN-fused-like weights as one flat f32 array.
 
-    Unit-fan-in normal weights, then the per-channel scale/shift stored in
-    data/synthetic_calib.npz (w' = w*scale, b' = b*scale + shift; produced
-    offline by tests/golden/make_yolo_scales.py), so every conv's
-    pre-activation is O(1) like a trained model's fused BN output and a road
-    frame yields a few hundred NMS candidates."""
+    Base weights (base_weights: He-normal, for some variants mixed with a
+    smooth part, data/synthetic_calib.npz "<variant>/smooth"), then the
+    per-channel scale/shift stored in data/synthetic_calib.npz (w' =
+    w*scale, b' = b*scale + shift; produced offline by
+    tests/golden/make_yolo_scales.py), so every conv's pre-activation is O(1)
+    like a trained model's fused BN output and a road frame yields a few
+    hundred NMS candidates."""
     rng = np.random.default_rng(seed)
     parts = []
     with np.load(_CALIB, allow_pickle=False) as cal:
-        for name, cin, cout, k, s, act in conv_list(variant):
-            w = rng.normal(0, 1 / np.sqrt(cin * k * k), size=(cout, cin, k, k)).astype(np.float32)
-            b = rng.normal(0, 0.05, size=(cout,)).astype(np.float32)
+        smooth = float(cal[f"{variant}/smooth"]) if f"{variant}/smooth" in cal.files else 0.0
+        for i, (name, cin, cout, k, s, act) in enumerate(conv_list(variant)):
+            w, b = base_weights(rng, seed, i, cin, cout, k, smooth)
             sc = cal[f"{variant}/{name}/scale"].astype(np.float32)
             sh = cal[f"{variant}/{name}/shift"].astype(np.float32)
             parts += [(w * sc[:, None, None, None]).ravel(), b * sc + sh]

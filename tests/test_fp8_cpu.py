@@ -36,6 +36,24 @@ def test_e4m3_matches_torch_cast():
     np.testing.assert_array_equal(ours, theirs)
 
 
+def test_quant_fp8_equals_code_table():
+    """quant_fp8 (torch's float8_e4m3fn cast after saturation) against the
+    code-table rounding on every representable value, every midpoint (ties
+    to even), the subnormal range, saturation and signed zeros, at several
+    power-of-two buffer scales."""
+    pos = Y.e4m3_table()[:127]
+    mid = (pos[:-1] + pos[1:]) / 2
+    rng = np.random.default_rng(3)
+    x = np.concatenate([pos, -pos, mid, -mid, rng.normal(0, 60, 50000),
+                        rng.uniform(-0.03, 0.03, 50000), [0.0, -0.0, 448.0, 470.0, 1e7, -1e7]])
+    for s in (2.0 ** -6, 1.0, 2.0 ** 3):
+        xs = (x * s).astype(np.float32)
+        ref = Y.e4m3_value(Y.e4m3_code(xs.astype(np.float64) / s)) * s
+        got = Y.quant_fp8(torch.from_numpy(xs), s).double().numpy()
+        np.testing.assert_array_equal(got, ref)
+        assert (np.signbit(got) == np.signbit(ref)).all()
+
+
 def test_fp8_scale_rule_matches_native():
     from rvs_amd import _lib
     lib = _lib.load()

@@ -19,11 +19,11 @@ configs[4]: "YOLOv8m 1280x1280 fp8 MFMA conv path").
     tools/fp8_scale_probe.hip: |err| up to 2^-11.8 of sum |products| within
     one 16x16x32 instruction, 2^-12.5 for the block-scaled 16x16x128), so
     ~0.3 % of each layer's codes land one step from the oracle's, and the
-    synthetic network in fp8 is chaotic under such flips: the ORACLE
-    ITSELF, given a 3e-5 relative perturbation before every rounding, keeps
-    50 % / 39 % of its detections at IoU >= 0.9 (75 % / 66 % at IoU >= 0.5)
-    and moves class scores by 0.048 at p99.9 (YOLOv8n 640x640).
-    The GPU sits at that floor; the bars below are set under it.
+    plain He-normal synthetic network is chaotic in fp8 under such flips
+    (the oracle itself keeps ~21-50 % of its detections at IoU >= 0.9 under
+    a 3e-5..3e-4 relative perturbation before every rounding); YOLOv8m's
+    synthetic weights carry a channel-coherent share that makes them
+    ordered (95-97.5 %), so its network-level bar is 90 %.
   * Config 5 geometry (YOLOv8m, 1280x1280, fog frames): runs, the NMS on the
     GPU's own raw prediction is bit-exact against the restated NMS, and the
     fp8 detections track the bf16 plan's.
@@ -242,6 +242,21 @@ def _match(a, b, iou=0.9, min_score=0.27):
 
 @pytest.mark.parametrize("H,W,variant", [(1080, 1920, 0), (640, 640, 2)])
 def test_fp8_network_matches_fp8_oracle(cuda, H, W, variant):
+    """Whole fp8 network against YoloRef(quant="fp8") with the GPU's own
+    per-buffer scales, and against the fp32 network.
+
+    YOLOv8m (config 5's model) runs weights with a channel-coherent share
+    (tests/golden/make_yolo_scales.py SMOOTH[2] = 0.25): the fp8 oracle
+    keeps 95-97.5 % of its own detections (class, IoU >= 0.9) under a 3e-5 /
+    3e-4 relative perturbation of every activation before its rounding
+    (tools/fp8_calib_study.py), so the GPU must match >= 90 % of the fp8
+    oracle's detections at IoU >= 0.9 and vice versa, and >= 80 % of its
+    detections must have an fp32 detection of the same class at IoU >= 0.5
+    (fp8 rounding lowers scores: fp32 has ~1.5x the detections; measured
+    on the CPU oracles 95 %).  YOLOv8n keeps the plain He-normal weights its
+    bf16 bench and tests use; those are chaotic in fp8 (the oracle keeps 21 %
+    of its detections under the same perturbation), so only loose bars
+    apply there."""
     B, keep = 2, [0, 2, 3, 5, 7]
     eng, flat = _engine(variant, H, W, B, cuda, seed=0, classes_keep=keep)
     fr = np.stack([cpu.median(cpu.clahe_ycrcb(road_frame(H, W, seed=20 + b)), 3)
@@ -271,8 +286,13 @@ def test_fp8_network_matches_fp8_oracle(cuda, H, W, variant):
           f"{ds.max():.4f}; box within 1px+1% {frac_box:.5f}; dets matched vs fp8 oracle "
           f"{h1}/{t1}, {h2}/{t2} (IoU 0.5: {l1}/{n1}, {l2}/{n2}); vs fp32 oracle {f1}/{u1}, "
           f"{f2}/{u2} (IoU 0.5: {k1}/{m1}, {k2}/{m2})")
-    assert n1 > 0 and l1 >= 0.4 * n1 and l2 >= 0.4 * n2
-    assert np.percentile(ds, 99.9) <= 0.15
+    assert t1 > 0 and t2 > 0
+    if variant == 2:
+        assert h1 >= 0.9 * t1 and h2 >= 0.9 * t2
+        assert k2 >= 0.8 * m2
+    else:
+        assert n1 > 0 and l1 >= 0.4 * n1 and l2 >= 0.4 * n2
+        assert np.percentile(ds, 99.9) <= 0.15
     eng.close()
 
 
@@ -307,6 +327,8 @@ def test_fp8_config5_fog_1280(cuda):
     (h1, t1), (h2, t2) = _match(got16, got8, 0.5), _match(got8, got16, 0.5)
     print(f"config5 fp8 vs bf16 plan (IoU 0.5): {h1}/{t1} bf16 dets matched, {h2}/{t2} fp8 "
           f"dets matched; IoU 0.9: {_match(got16, got8)}, {_match(got8, got16)}")
-    assert t1 > 0 and h1 >= 0.3 * t1 and h2 >= 0.3 * t2
+    # fp8 rounding lowers scores (the bf16 plan keeps more detections): most
+    # fp8 detections must be bf16 ones
+    assert t1 > 0 and t2 > 0 and h2 >= 0.8 * t2
     eng.close()
     e16.close()
