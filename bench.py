@@ -83,6 +83,9 @@ def parse_args(argv=None):
     ap.add_argument("--pair", type=int, default=int(os.environ.get("RV_PAIR", 4)),
                     help="steps per pipeline unit (one forward over pair x streams frames); the "
                          "largest divisor of --steps not above it is used")
+    ap.add_argument("--warm-runs", type=int, default=int(os.environ.get("RV_WARM_RUNS", 1)),
+                    help="untimed runs of the recorded schedule over the timed frames before the "
+                         "timed region (warm-up of the schedule itself)")
     ap.add_argument("--no-consumer", action="store_true",
                     help="do not build the Detection lists inside the timed region")
     ap.add_argument("--no-autotune", action="store_true",
@@ -202,21 +205,26 @@ class BenchJob:
                                        [self.ts[Wm + k] for k in range(K)], mode=a.exec_mode,
                                        sync=a.sync)
             self.records = self.runner.records
+            if a.warm_runs > 0:
+                # the SORT state is restored afterwards, so the timed run sees
+                # exactly the tracks the warm-up steps left
+                saved = eng.tracker.state[0].clone()
+                for _ in range(a.warm_runs):
+                    self.runner.run()
+                eng.tracker.state[0].copy_(saved)
         torch.cuda.synchronize()
 
     def _consume(self, wait_step, materialise: bool):
         """The consumer: every step's List[Detection] per stream, built as
         soon as that step's record has been handed back (materialise=False:
         only the host time each step became available)."""
-        from rvs_amd.handback import to_detections
         names, n_det, busy, done = self.eng.names, 0, 0.0, []
         for k, rec in enumerate(self.records):
             wait_step(k)
             t = time.perf_counter()
             done.append(t)
             if materialise:
-                n, rows = rec.arrays()
-                n_det += sum(len(x) for x in to_detections(n, rows, names))
+                n_det += sum(len(x) for x in rec.detections(names))
                 busy += time.perf_counter() - t
         self.cons = {"detections": n_det, "busy_s": busy, "end": time.perf_counter(),
                      "done": done}
@@ -542,12 +550,19 @@ def main(argv=None):
     torch.cuda.set_device(dev)
 
     job = BenchJob(args, rank, dev)
-    t = rank_job(job, dev)
+    if os.environ.get("RV_BENCH_DEVICE_FIRST"):  # A/B probe: the device-only run first
+        job.warmup()
+        job.prepare()
+        rank_job_again(job, dev)
+        from rvs_amd.shard import timed_job
+        t = timed_job(job.run, job.sync, job.units, dev)
+    else:
+        t = rank_job(job, dev)
     elapsed, value = t["elapsed_s"], t["value"]
     K, S = job.K, job.S
     cons = job.cons
     handback = {"consumer": ("in the timed region: a host thread builds every step's "
-                             "List[Detection] per stream (rvs_amd.handback.to_detections) as "
+                             "List[Detection] per stream (rvs_amd.handback.Record.detections) as "
                              "soon as the step's record is handed back"
                              if job.consume == "consume" else "off"),
                 "record_bytes_per_step": job.records[0].nbytes}

@@ -22,7 +22,7 @@ from .detect.types import Detection
 from .detect.weights import COCO80, variant_of, weights_from_config
 from .detect.yolo_hip import YoloEngine
 from .geometry import GroundProjector, build_projector
-from .handback import Record, handback, to_detections
+from .handback import Record, handback
 from .preprocess import PreprocessPipeline
 from .track.sort_hip import MultiStreamSort
 
@@ -191,8 +191,7 @@ class RoadVisionEngine:
                                    "results(out) before the next step(), or pass step() its own "
                                    "Record")
             torch.cuda.synchronize(self.device)
-            n, rows = out["record"].arrays()
-            return to_detections(n, rows, self.names)
+            return out["record"].detections(self.names)
         d = out["dets"].cpu().numpy()
         n = out["det_n"].cpu().numpy()
         tid = out["track_id"].cpu().numpy()

@@ -18,6 +18,11 @@ import torch
 from . import _lib
 from .detect.types import Detection
 
+try:  # the C builder of the Detection lists (csrc/handback_py.c, built by the csrc Makefile)
+    from . import _rvhandback
+except ImportError:  # pragma: no cover - a checkout without the build: the numpy version
+    _rvhandback = None
+
 ROW = np.dtype([("x1", "<f4"), ("y1", "<f4"), ("x2", "<f4"), ("y2", "<f4"), ("conf", "<f4"),
                 ("cls", "<i4"), ("track_id", "<i4"), ("pad", "<i4"), ("dist", "<f8"),
                 ("speed", "<f8")])
@@ -40,6 +45,14 @@ class Record:
         self.nbytes = record_bytes(self.S, self.dmax)
         self.host = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True) if host else None
         self.seq = 0  # hand-backs issued into this record (RoadVisionEngine.results checks it)
+
+    def detections(self, names: Sequence[str]) -> List[List[Detection]]:
+        """The reference's Detection lists of this record (the caller must
+        have synchronised the stream that filled it): built in C
+        (_rvhandback) when available, else by to_detections."""
+        if _rvhandback is not None:
+            return _rvhandback.build(self.host.numpy(), self.S, self.dmax, list(names), Detection)
+        return to_detections(*self.arrays(), names)
 
     def arrays(self):
         """(counts (S,), rows (S, dmax) structured) views of the host record.

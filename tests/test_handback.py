@@ -54,3 +54,39 @@ def test_to_detections_matches_rowwise_construction():
 def test_to_detections_empty():
     rows = np.zeros((3, 4), ROW)
     assert to_detections(np.zeros(3, np.int32), rows, COCO80) == [[], [], []]
+
+
+def _record_bytes(n, rows):
+    S, dmax = rows.shape
+    hdr = (S * 4 + 15) & ~15
+    buf = np.zeros(hdr + rows.nbytes, np.uint8)
+    buf[:4 * S].view(np.int32)[:] = n
+    buf[hdr:] = rows.reshape(-1).view(np.uint8)
+    return buf
+
+
+def test_c_builder_matches_python():
+    """csrc/handback_py.c (Record.detections' builder) builds exactly the
+    objects of to_detections from the raw record bytes (the 16-B-padded
+    count header, then the 48-B rows)."""
+    from rvs_amd import handback
+    assert handback._rvhandback is not None, "the C builder is not built (make -C csrc)"
+    rng = np.random.default_rng(11)
+    for S, dmax in ((5, 9), (32, 100), (1, 1)):
+        rows = np.zeros((S, dmax), ROW)
+        for f in ("x1", "y1", "x2", "y2", "conf"):
+            rows[f] = rng.uniform(-5, 2000, (S, dmax)).astype(np.float32)
+        rows["cls"] = rng.integers(-2, 84, (S, dmax))
+        rows["track_id"] = rng.integers(-1, 40, (S, dmax))
+        rows["dist"] = np.where(rng.random((S, dmax)) < 0.3, np.nan, rng.uniform(0, 9, (S, dmax)))
+        rows["speed"] = np.where(rng.random((S, dmax)) < 0.5, np.nan, rng.uniform(0, 9, (S, dmax)))
+        n = rng.integers(-2, dmax + 3, S).astype(np.int32)
+        got = handback._rvhandback.build(_record_bytes(n, rows), S, dmax, list(COCO80), Detection)
+        want = to_detections(n, rows, COCO80)
+        assert got == want
+        for a, b in zip(sum(got, []), sum(want, [])):
+            assert vars(a) == vars(b)
+            assert all(type(getattr(a, f)) is type(getattr(b, f)) for f in vars(b))
+    import pytest
+    with pytest.raises(ValueError):
+        handback._rvhandback.build(np.zeros(10, np.uint8), 2, 2, list(COCO80), Detection)

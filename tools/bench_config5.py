@@ -38,7 +38,9 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--autotune", type=int, default=1)
-    p.add_argument("--cpu-frames", type=int, default=16, help="0 skips the CPU baseline")
+    p.add_argument("--cpu-frames", type=int, default=1,
+                   help="CPU baseline frames (the full fog oracle takes ~1 min per 1280x1280 frame); "
+                        "0 skips it")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--fog", default="full", choices=["full", "core"],
                    help="full: the reference's whole synthesize with tools/fog_batch.py's "
@@ -65,7 +67,12 @@ def conv_profile(eng, lb, n=3):
     return float(ms[v].sum()) / max(nf, 1), float(fl[v].sum()), float(by[v].sum()), int(v.sum())
 
 
-def cpu_baseline(clean_host, flat, frames, threads):
+def cpu_baseline(clean_host, flat, frames, threads, fog="full"):
+    """The CPU restatement of the same step on a bounded sample: the fog
+    oracle (fog="full": fog_frame_full, every stage of the reference's
+    synthesize, src/augment/fog.py:227-299, with tools/fog_batch.py:20-28's
+    settings -- the GPU leg's work; "core": the scattering core only),
+    letterbox, torch-CPU fp32 YOLOv8m, restated NMS."""
     from oracle import cpu, fog_ref, yolo_ref
     torch.set_num_threads(threads)
     model = yolo_ref.YoloRef(2, flat)
@@ -75,8 +82,14 @@ def cpu_baseline(clean_host, flat, frames, threads):
     t0 = time.perf_counter()
     for i in range(frames):
         a = time.perf_counter()
-        prm = fog_ref.draw(rng, H, W, level="medium", rain=True)
-        img = fog_ref.fog_frame(clean_host[i % len(clean_host)], prm, rain_p=0.002)
+        if fog == "full":
+            prm = fog_ref.draw_full(rng, H, W, level="medium", rain=True)
+            img = fog_ref.fog_frame_full(clean_host[i % len(clean_host)], prm, y_h_ratio=0.42,
+                                         softness_ratio=0.07, global_veil=0.5,
+                                         depth_blur_max=4.0, rain_p=0.002)
+        else:
+            prm = fog_ref.draw(rng, H, W, level="medium", rain=True)
+            img = fog_ref.fog_frame(clean_host[i % len(clean_host)], prm, rain_p=0.002)
         lb = cpu.letterbox(img, cpu.letterbox_geometry(H, W, 1280))[None]
         b = time.perf_counter()
         raw = model.forward(yolo_ref.preprocess(lb)).numpy()
@@ -88,9 +101,12 @@ def cpu_baseline(clean_host, flat, frames, threads):
     return {"value": round(frames / dt, 4), "unit": "frames/s", "cores": threads, "kind": "port",
             "host_cpus": os.cpu_count(), "stage_s_per_frame": {
                 k: round(v / frames, 3) for k, v in zip(["fog+letterbox", "yolov8m_fp32", "nms"], t)},
-            "sample": f"{frames} frame(s) of 1280x1280: oracle fog_frame (numpy f32, the scattering "
-                      f"core; the full filter chain is not timed on the CPU) + torch-CPU "
-                      f"fp32 YOLOv8m ({threads} threads) + restated NMS; {dt:.1f} s"}
+            "sample": f"{frames} frame(s) of 1280x1280: oracle "
+                      + ("fog_frame_full (numpy f32, every stage of the reference's synthesize "
+                         "with tools/fog_batch.py's settings)" if fog == "full" else
+                         "fog_frame (numpy f32, the scattering core)")
+                      + f" + torch-CPU fp32 YOLOv8m ({threads} threads) + restated NMS; "
+                      f"{dt:.1f} s"}
 
 
 def main():
@@ -172,7 +188,7 @@ def main():
     }
     if args.cpu_frames > 0:
         thr = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0)) or min(16, os.cpu_count())
-        out["cpu_baseline"] = cpu_baseline(clean_host, flat, args.cpu_frames, thr)
+        out["cpu_baseline"] = cpu_baseline(clean_host, flat, args.cpu_frames, thr, args.fog)
     print(json.dumps(out))
 
 
