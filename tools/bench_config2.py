@@ -9,18 +9,20 @@ copy at that size) on u8 frames resident in HBM:
   forward_eager   letterbox + YOLOv8n forward + fused decode, launched from
                   the host each call (~40 launches)
   detect_eager    the same + NMS / scale_boxes / class filter
-  detect_graph    letterbox + forward + NMS captured once as a HIP graph and
-                  replayed (the serving form: one launch per frame)
-  chain_graph     the whole per-frame chain (CLAHE + median + letterbox +
+  detect_native   letterbox + forward + NMS recorded once as a native launch
+                  list (rvs_amd.schedule.Schedule) and issued with one C call
+                  per frame (the serving form; no HIP graph capture, which
+                  crashed intermittently in r02: DESIGN.md §3)
+  chain_native    the whole per-frame chain (CLAHE + median + letterbox +
                   forward + NMS + SORT + result hand-back to pinned host) as
-                  one captured step of RoadVisionEngine(S=1)
+                  one recorded step of RoadVisionEngine(S=1)
   infer_host      YOLOHip.infer(np.ndarray) exactly as the reference calls
                   it: H2D of the frame, the device path, D2H and Detection
                   construction
 
 Each is timed per call (host clock, synchronised after every call: a
 latency, not a throughput) over --iters calls after --warmup; the JSON line
-reports median / p90 / p99 in ms.  `roofline` prices the graph-replayed
+reports median / p90 / p99 in ms.  `roofline` prices the launch-list
 forward against the dense bf16 MFMA peak (8.742 GFLOP per 640^2 frame,
 SURVEY 8(d)); at batch 1 the forward is ~40 dependent launches of a few
 microseconds each, so the fraction is a latency statement.  cpu_baseline =
@@ -120,23 +122,19 @@ def main():
                                        args.warmup))
     res["detect_eager"] = stats(timed(lambda: eng.run(frame), args.iters, args.warmup))
 
-    s = torch.cuda.Stream(dev)
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
+    from rvs_amd.schedule import Schedule
+    g = Schedule()
+    with g.recording():
         eng.run(frame)
-    torch.cuda.current_stream().wait_stream(s)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        eng.run(frame)
-    res["detect_graph"] = stats(timed(g.replay, args.iters, args.warmup))
-    gf = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(gf):
+    res["detect_native"] = stats(timed(g.run, args.iters, args.warmup))
+    gf = Schedule()
+    with gf.recording():
         eng.forward_raw(eng.letterbox(frame))
-    res["forward_graph"] = stats(timed(gf.replay, args.iters, args.warmup))
-    fwd_dev_ms = device_ms(gf.replay)
-    det_dev_ms = device_ms(g.replay)
+    res["forward_native"] = stats(timed(gf.run, args.iters, args.warmup))
+    fwd_dev_ms = device_ms(gf.run)
+    det_dev_ms = device_ms(g.run)
 
-    # the whole per-frame chain, one stream, one captured step
+    # the whole per-frame chain, one stream, one recorded step
     cfg = load_config()
     cfg["detect"]["weights"] = "synthetic"
     rve = RoadVisionEngine(cfg, 1, (H, W), device=dev, weights=flat)
@@ -145,14 +143,18 @@ def main():
     for _ in range(3):
         rve.step(frame, ts)
     torch.cuda.synchronize()
-    gc, out = rve.capture(frame, ts)
+    gc = Schedule()
+    with gc.recording():
+        out = rve.step(frame, ts)
     k = [0]
 
     def chain():
         ts.fill_(k[0] / 30.0)
         k[0] += 1
-        gc.replay()
-    res["chain_graph"] = stats(timed(chain, args.iters, args.warmup))
+        gc.run()
+    res["chain_native"] = stats(timed(chain, args.iters, args.warmup))
+    torch.cuda.synchronize()
+    out["seq"] = out["record"].seq
     n_chain = len(rve.results(out)[0])
 
     det = YOLOHip({"model": "yolov8n.pt", "weights": "synthetic", "classes_keep": keep})
@@ -162,19 +164,19 @@ def main():
     res["infer_host"] = stats(timed(lambda: det.infer(host), args.iters // 2, args.warmup))
     n_det = len(det.infer(host))
 
-    lat = res["detect_graph"]["median_ms"]
+    lat = res["detect_native"]["median_ms"]
     tf = GFLOP / (fwd_dev_ms * 1e-3) / 1e3
     line = {
-        "metric": "YOLOv8n 640x640 batch=1 detect latency (letterbox+forward+NMS, graph replay)",
+        "metric": "YOLOv8n 640x640 batch=1 detect latency (letterbox+forward+NMS, native launch list)",
         "value": lat, "unit": "ms", "n_gpus": 1, "steps": args.iters, "warmup": args.warmup,
         "higher_is_better": False, "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (one 640x640 road frame, synthetic YOLOv8n weights)",
         "config": {"workload": "configs[1]: YOLOv8n 640x640 batch=1 bf16", "batch": 1,
                    "imgsz": 640, "autotune": bool(args.autotune)},
         "latency": res,
-        "device_ms_back_to_back": {"forward_graph": round(fwd_dev_ms, 4),
-                                   "detect_graph": round(det_dev_ms, 4)},
-        "roofline": {"kernel": "YOLOv8n forward, graph replay back to back (one frame)",
+        "device_ms_back_to_back": {"forward_native": round(fwd_dev_ms, 4),
+                                   "detect_native": round(det_dev_ms, 4)},
+        "roofline": {"kernel": "YOLOv8n forward, launch list back to back (one frame)",
                      "bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16,
                      "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16, 5), "traffic": None},
         "detections": {"infer_host": n_det, "chain": n_chain},
