@@ -285,6 +285,17 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------------
 __device__ __attribute__((aligned(64))) uint4 g_zero16[4];
 
+// Buffer-resource LDS-DMA (conv_patch_kernel): dword3 of the descriptor
+// for a raw (stride 0) buffer on gfx950, and the voffset that the range
+// check (voffset + soffset against num_records, checked on the GPU:
+// tools/probe_buffer_oob.hip) always rejects -- such a load writes zeros.
+constexpr int kRsrcFlags = 0x00020000;
+constexpr uint32_t kOOB = 0x80000000u;
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
+                                           (int)voff, soff, 0, 0);
+}
+
 struct PatchGeo {
   int C, R;        // output tile cols / rows (R*C <= 64*NR)
   int G;           // input-channel chunks per pipeline stage
@@ -594,49 +605,70 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
       dq[m] = ws * a.s_in;
     }
   }
-  int poff[MAXP];
+  // Patch and weight DMA through buffer resources (buffer_load ... lds):
+  // every DMA instruction's per-lane byte offset is computed once -- per
+  // tile for the patch, per kernel for the weights --, the chunk offset
+  // rides in the scalar soffset, and out-of-image pixels / rows beyond Cout
+  // read zeros from the range check (voffset kOOB).  So a chunk step issues
+  // its DMA with no address VALU; the tile-invariant lane geometry (patch
+  // row, column, source quarter of every slot) is computed once per kernel.
   uint32_t tailbad = 0;  // bit it: this lane's quarter is >= Cin in the last chunk
-  const uint8_t* img = (const uint8_t*)a.in;
+  // slot it's patch row / column / source quarter: py | px << 12 | sq << 24;
+  // a slot beyond the patch gets row 4095, which no map reaches (range check)
+  int lgeo[MAXP];
+#pragma unroll
+  for (int it = 0; it < MAXP; ++it) {
+    const int L = 64 * (wave + 4 * it) + lane;
+    const int pix = L / SL, q = L - SL * pix;
+    const int py = (int)(((float)pix + 0.5f) * inv_pw);
+    const int sc = pix - py * g.PW;  // stored column
+    const int he = (g.PW + 1) >> 1;
+    const int px = S == 1 ? sc : (sc < he ? 2 * sc : 2 * (sc - he) + 1);
+    const int sq = q ^ swzq<F8>(sc);  // source quarter of slot q
+    lgeo[it] = (pix < npp ? py : 4095) | (px << 12) | (sq << 24);
+    if ((nch - 1) * CC + sq * (16 / EB) >= Cin) tailbad |= 1u << it;
+  }
+  const bool has_tail = Cin % CC != 0;
+  uint32_t voff[MAXP];
+  __amdgpu_buffer_rsrc_t img_rsrc;
+  const int pix_bytes = a.in_cs * EB;
   auto prep_tile = [&](int ti) {
     const int b = ti / tiles_img;
     const int r = ti - b * tiles_img;
     const int ty = r / g.tiles_x, tx = r - (r / g.tiles_x) * g.tiles_x;
     const int iy0 = ty * g.R * S - pad, ix0 = tx * g.C * S - pad;
-    img = (const uint8_t*)a.in + ((size_t)b * a.Hin * a.Win * a.in_cs + in_co) * EB;
-    tailbad = 0;
+    const uint8_t* base = (const uint8_t*)a.in + ((size_t)b * a.Hin * a.Win * a.in_cs + in_co) * EB;
+    img_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0,
+                                                 (a.Hin * a.Win * a.in_cs - in_co) * EB, kRsrcFlags);
 #pragma unroll
     for (int it = 0; it < MAXP; ++it) {
-      const int L = 64 * (wave + 4 * it) + lane;
-      const int pix = L / SL, q = L - SL * pix;
-      const int py = (int)(((float)pix + 0.5f) * inv_pw);
-      const int sc = pix - py * g.PW;  // stored column
-      const int he = (g.PW + 1) >> 1;
-      const int px = S == 1 ? sc : (sc < he ? 2 * sc : 2 * (sc - he) + 1);
-      const int iy = iy0 + py, ix = ix0 + px;
-      const int sq = q ^ swzq<F8>(sc);  // source quarter of slot q
-      const bool ok = pix < npp && (unsigned)iy < (unsigned)a.Hin &&
-                      (unsigned)ix < (unsigned)a.Win;
-      poff[it] = ok ? (iy * a.Win + ix) * a.in_cs * EB + sq * 16 : -1;
-      if ((nch - 1) * CC + sq * (16 / EB) >= Cin) tailbad |= 1u << it;
+      const int gg = lgeo[it];
+      const int iy = iy0 + (gg & 4095), ix = ix0 + ((gg >> 12) & 4095);
+      const bool ok = (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+      // branchless select: an out-of-image slot reads zeros (kOOB)
+      const uint32_t off = (uint32_t)(iy * a.Win + ix) * (uint32_t)pix_bytes + ((gg >> 24) & 3) * 16;
+      const uint32_t m = ok ? 0u : 0xFFFFFFFFu;
+      voff[it] = (off & ~m) | (kOOB & m);
     }
   };
   // weight DMA: instruction j moves (row, tap) pairs 16 j .. 16 j + 15, a
-  // 16-B quarter of chunk c per lane; offsets are recomputed per call
-  // (constant divisor, no registers held across the loop)
+  // 16-B quarter of chunk c per lane
+  const __amdgpu_buffer_rsrc_t w_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(wts + (size_t)wc0 * Kp * EB), 0, (wcout_pad - wc0) * Kp * EB, kRsrcFlags);
+  uint32_t wvoff[MAXW];
+#pragma unroll
+  for (int it = 0; it < MAXW; ++it) {
+    const int j = wave + 4 * it;
+    const int pr = j * 16 + (lane >> 2);
+    const int row = pr / T2, tap = pr - (pr / T2) * T2;
+    const int q = (lane & 3) ^ swzq<F8>(row);
+    wvoff[it] = wc0 + row < wcout_pad ? (uint32_t)((row * Kp + tap * cin_pad) * EB + q * 16) : kOOB;
+  }
   auto dma_weights = [&](int c, uint8_t* Wl) {
 #pragma unroll
     for (int it = 0; it < MAXW; ++it) {
       const int j = wave + 4 * it;
-      if (j < WJ) {
-        const int pr = j * 16 + (lane >> 2);
-        const int row = pr / T2, tap = pr - (pr / T2) * T2;
-        const int q = (lane & 3) ^ swzq<F8>(row);
-        const int co = wc0 + row;
-        const void* src = co < wcout_pad
-                              ? (const void*)(wts + ((size_t)co * Kp + tap * cin_pad) * EB + q * 16 + c * 64)
-                              : (const void*)g_zero16;
-        __builtin_amdgcn_global_load_lds(src, (void*)(Wl + j * 1024), 16, 0, 0);
-      }
+      if (j < WJ) dma16(w_rsrc, Wl + j * 1024, wvoff[it], c * 64);
     }
   };
   auto stage = [&](int grp, int buf) {
@@ -644,15 +676,13 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
       const int c = grp * G + gi;
       if (c >= nch) break;
       uint8_t* P = stages + buf * stage_bytes + gi * chunk_bytes;
-      const uint32_t bad = c == nch - 1 ? tailbad : 0u;
+      const bool tail = has_tail && c == nch - 1;
 #pragma unroll
       for (int it = 0; it < MAXP; ++it) {
         const int j = wave + 4 * it;
         if (j < g.pinst) {
-          const void* src = (poff[it] >= 0 && !((bad >> it) & 1))
-                                ? (const void*)(img + poff[it] + c * 64)
-                                : (const void*)g_zero16;
-          __builtin_amdgcn_global_load_lds(src, (void*)(P + j * 1024), 16, 0, 0);
+          const uint32_t v = tail && ((tailbad >> it) & 1) ? kOOB : voff[it];
+          dma16(img_rsrc, P + j * 1024, v, c * 64);
         }
       }
       if constexpr (!RESW) dma_weights(c, P + g.p_bytes);

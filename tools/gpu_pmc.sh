@@ -21,11 +21,3 @@ python3 tools/pmc_traffic.py "$OUT/pmc_traffic.json" "$OUT"/pass1.csv "$OUT"/pas
 python3 tools/pmc_family.py "$OUT/pmc_family.json" "$OUT"/pass*.csv > "$OUT/pmc_family.txt"
 rm -f "$OUT"/pass*.csv  # large (every dispatch of the run); the report keeps the last step
 tail -3 "$OUT/report.txt"
-# per-kernel time breakdown of the bench step (graph replays) from a kernel trace
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/tr" -o t -- \
-  python3 tools/trace_step.py > "$OUT/trace_step.log" 2>&1
-find "$OUT/tr" -name "*kernel_trace.csv" -exec mv {} "$OUT/trace.csv" \;
-rm -rf "$OUT/tr"
-python3 tools/kernel_breakdown.py "$OUT/trace.csv" 19 > "$OUT/kernel_breakdown.txt"
-rm -f "$OUT/trace.csv"
-head -30 "$OUT/kernel_breakdown.txt"
