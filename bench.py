@@ -329,6 +329,7 @@ def _conv_pass(job, mode: str, tags):
     if table:  # per-launch table of this pass (tools: per-layer roofline)
         from rvs_amd.detect.weights import conv_list
         names = [c[0] for c in conv_list(eng.variant)]
+        names[0] = "stem (model.0 + model.1 + model.2.cv1)"  # slot n - 1: the fused stem
         with open(f"{table}_{mode}.json", "w") as f:
             json.dump({"mode": mode, "forwards": int(nf), "batch": eng.S * eng.pair,
                        "launches": [{"conv": names[int(cv[i])], "us": ms[i] / max(nf, 1) * 1e3,
@@ -364,7 +365,8 @@ def pmc_traffic() -> dict:
 
 def conv_roofline(job, mode: str) -> dict:
     """Roofline of the conv family (every conv launch of a step:
-    conv_patch_kernel, conv1x1_direct_kernel, c2f_chain_kernel) against
+    conv_patch_kernel, conv1x1_direct_kernel, c2f_chain_kernel, and the fused
+    stem_kernel = model.0 + model.1 + model.2.cv1) against
     SURVEY §8(d)'s MFMA bound: achieved = the family's algorithmic FLOPs per
     step / its HIP-event-timed duration per step (rv_yolo_profile: events on
     the launch stream around every conv launch).
@@ -398,6 +400,7 @@ def conv_roofline(job, mode: str) -> dict:
         return {"error": "no event timings"}
     main = "eager" if "eager" in res else "overlap"
     out = {"kernel": "conv family: conv_patch_kernel + conv1x1_direct_kernel + c2f_chain_kernel "
+                     "+ stem_kernel "
                      "(all YOLOv8n conv launches of a step; HIP events on the launch stream)",
            "timing": main + (" (one pipeline unit at a time: each launch alone, on the timed "
                              "region's forward batch)" if main == "eager" else

@@ -69,22 +69,29 @@ int launch_conv_cfg(const ConvArgs& a, const ConvCfg& c, hipStream_t s);
 bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c);
 int conv_candidates(const ConvArgs& a, ConvCfg* out, int cap);
 
-// First conv (3 -> C0, k3 s2 p1) straight from the u8 BGR letterboxed
-// frame, f32 arithmetic: x = u8/255 with the RGB order of the reference
-// (predictor preprocess: im[..., ::-1] / 255).  w: [C0][3 rgb][3][3] f32.
-int launch_conv0(const uint8_t* img, int B, int H, int W, const float* w, const float* bias,
-                 int C0, bf16_t* out, int out_cs, hipStream_t s);
+// First conv (3 -> C0, k3 s2, p1) straight from the u8 BGR letterboxed
+// frame (the reference's predictor preprocess im[..., ::-1] / 255 folded into
+// the weights), on i8 MFMAs over the window bytes with exact i32 sums; the
+// weights in the integer form yolo.hip's packer writes (pack_conv0q).
+struct Conv0Q {
+  const int8_t* d;   // [3][C0][64] balanced base-256 digits of Q (k = 16 ky + 3 kx + ch, BGR)
+  const float* s;    // [C0] value scale
+  const float* b;    // [C0] bias
+  const int32_t* c;  // [3][C0] 128 sum_k D_i[k]: digit i's accumulator start
+};
+int launch_conv0(const uint8_t* img, int B, int H, int W, const Conv0Q& q, int C0, bf16_t* out,
+                 int out_cs, hipStream_t s);
 // The same with an fp8 output (codes of value / s_out, channel stride out_cs
 // bytes).
-int launch_conv0_fp8(const uint8_t* img, int B, int H, int W, const float* w, const float* bias,
-                     int C0, uint8_t* out, int out_cs, float s_out, hipStream_t s);
+int launch_conv0_fp8(const uint8_t* img, int B, int H, int W, const Conv0Q& q, int C0,
+                     uint8_t* out, int out_cs, float s_out, hipStream_t s);
 
 // conv0 and model.1 (C0 = 16 -> C1 = 32, k3 s2) fused: the P1 map never
 // leaves LDS.  w1/b1: model.1's packed weights / bias; out (nullable): X1
 // (NHWC, channel stride out_cs).  w2/b2/out2 (nullable): the following 1x1
 // conv 32 -> 32 (model.2.cv1) run from the registers into out2 (channel
 // stride out2_cs), bit-identical to the unfused 1x1 kernels.
-int launch_stem(const uint8_t* img, int B, int H, int W, const float* w0, const float* b0, int C0,
+int launch_stem(const uint8_t* img, int B, int H, int W, const Conv0Q& q0, int C0,
                 const bf16_t* w1, const float* b1, int C1, bf16_t* out, int out_cs,
                 hipStream_t s, const bf16_t* w2 = nullptr, const float* b2 = nullptr,
                 bf16_t* out2 = nullptr, int out2_cs = 0);

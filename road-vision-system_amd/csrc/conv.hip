@@ -1298,28 +1298,100 @@ static int try_launch_patch(const ConvArgs& a, hipStream_t s, int* st) {
 // ---------------------------------------------------------------------------
 // conv0: 3 -> C0, k3 s2 p1, from letterboxed u8 BGR, SiLU, bf16 out.
 // ---------------------------------------------------------------------------
-// conv0 on MFMA.  GEMM view: D[cout][px] = sum_k W'[cout][k] X[k][px] with
-// k = ky*9 + kx*3 + ch over the 3x3 window's 27 BGR bytes (padded to 32)
-// and X the raw u8 values, exact in bf16.  The 1/255 scale and the BGR->RGB
-// channel order live in W' = w[cout][2-ch][ky][kx] / 255, split into three
-// bf16 parts (hi + mid + lo, three MFMAs), so the products carry the f32
-// weight's full 24-bit significand and accumulate in f32.
-// Workgroup = 8 x 64 output pixels; wave w owns the 16-pixel-wide column
-// strip w and its 8 rows (one 16-pixel MFMA group per row).  The
-// (17 x 129) x 3 byte input window is staged in LDS as u16 (bf16 bit
-// patterns), so a lane's 8 k-values are 8 ds_read_u16 at per-lane addresses
-// fixed for the whole block plus a compile-time per-row offset.
-constexpr int kC0TH = 8, kC0TW = 64;
-constexpr int kC0IW = (2 * kC0TW + 1) * 3;  // 387 bytes per input row
-constexpr int kC0RS = kC0IW + 5;            // LDS row stride (u16 elements, 8-B multiple)
+// conv0 on integer MFMA (v_mfma_i32_16x16x64_i8).  GEMM view: D[cout][px] =
+// sum_k Q[cout][k] x[k][px] over the 3x3 window's 27 BGR bytes,
+// k = 16 ky + 3 kx + ch (lane quad q supplies the 9 bytes of window row
+// ky = q; quad 3 and k % 16 >= 9 carry zero weights).  The window row is 9
+// contiguous bytes of the letterbox row, so a lane's B operand is three
+// dword loads, three v_alignbyte_b32 and an XOR 0x80 each (u8 x -> i8
+// x - 128): no per-byte conversion.  The weights are the integers Q =
+// round(V / s) of V = w[rgb][ky][kx] / 255 at 2^-23 of the channel's largest
+// |V| (yolo.hip pack_conv0q) in three balanced base-256 i8 digits, one MFMA
+// each, the accumulator started at 128 sum_k D_i[k] so it ends at
+// T_i = sum_k D_i[k] x[k] exactly (< 2^24, exact in f32).  The value is
+// s (65536 T0 + 256 T1 + T2) + b in f32 -- the f64 reference within 1 bf16
+// ulp (test_first_conv_sppf_and_decode).
+// Out-of-image window bytes read zeros through the buffer range check
+// (voffset kOOB), i.e. the zero padding of the normalised image.
+// ---------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+
+// raw window words of X0 map pixel (Y, X), lane quad q: lb row 2Y - 1 + q,
+// bytes 6X - 3 .. 6X + 5 of it inside the three dwords from its aligned base
+struct C0Win {
+  uint32_t w0, w1, w2;
+  int sh;
+};
+
+__device__ __forceinline__ C0Win conv0_window(__amdgpu_buffer_rsrc_t r, int Y, int X, int quad, int H,
+                                              int rowb, bool valid) {
+  const int row = 2 * Y - 1 + quad;
+  const int start = 6 * X - 3;
+  C0Win w;
+  w.sh = start & 3;
+  const bool ok = valid && quad < 3 && (unsigned)row < (unsigned)H;
+  const uint32_t vb = ok ? (uint32_t)(row * rowb + start - w.sh) : kOOB;
+  // X = 0: the dword before the window's first byte is the left padding
+  const uint32_t v0 = X > 0 ? vb : kOOB;
+  w.w0 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)v0, 0, 0);
+  w.w1 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)(vb + 4u), 0, 0);
+  w.w2 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)(vb + 8u), 0, 0);
+  return w;
+}
+
+__device__ __forceinline__ i32x4 conv0_bop(const C0Win& w) {
+  const uint32_t b0 = __builtin_amdgcn_alignbyte(w.w1, w.w0, w.sh) ^ 0x80808080u;
+  const uint32_t b1 = __builtin_amdgcn_alignbyte(w.w2, w.w1, w.sh) ^ 0x80808080u;
+  const uint32_t b2 = __builtin_amdgcn_alignbyte(w.w2, w.w2, w.sh) ^ 0x80808080u;
+  return i32x4{(int)b0, (int)b1, (int)b2, 0};
+}
+
+// the digits of cout rows 16 m + col (A operands) and the lane's 4 output
+// channels' scale / folded bias
+template <int MR>
+struct C0Wts {
+  i32x4 d[MR][3], c[MR][3];
+  f32x4 s[MR], b[MR];
+  __device__ __forceinline__ void load(const Conv0Q& q, int C0, int col, int quad) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        d[m][t] = *(const i32x4*)(q.d + ((size_t)t * C0 + 16 * m + col) * 64 + 16 * quad);
+        c[m][t] = *(const i32x4*)(q.c + (size_t)t * C0 + 16 * m + 4 * quad);
+      }
+      s[m] = *(const f32x4*)(q.s + 16 * m + 4 * quad);
+      b[m] = *(const f32x4*)(q.b + 16 * m + 4 * quad);
+    }
+  }
+};
+
+// one 16-pixel fragment: lane (col, quad) -> SiLU(conv0) of output channels
+// 16 m + 4 quad .. +3 of the fragment's pixel col
+template <int MR>
+__device__ __forceinline__ void conv0_frag(const C0Wts<MR>& W, const i32x4 X, f32x4 (&v)[MR]) {
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    i32x4 t[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) t[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(W.d[m][i], X, W.c[m][i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float u = fmaf((float)t[0][i], 65536.0f, (float)t[1][i] * 256.0f) + (float)t[2][i];
+      v[m][i] = silu(fmaf(W.s[m][i], u, W.b[m][i]));
+    }
+  }
+}
+
+// Unfused conv0: a workgroup is 4 x 64 output pixels; wave w owns row w,
+// 4 fragments of 16 pixels; the window loads of fragment j + 1 are in flight
+// while fragment j runs.
+constexpr int kC0TH = 4, kC0TW = 64;
 
 template <int MR, bool F8 = false>
 __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ img, int B, int H,
-                                                    int W, const float* __restrict__ w,
-                                                    const float* __restrict__ bias,
-                                                    void* __restrict__ out, int out_cs,
-                                                    float s_out = 1.f) {
-  __shared__ uint16_t xin[(2 * kC0TH + 1) * kC0RS];
+                                                    int W, Conv0Q q, void* __restrict__ out,
+                                                    int out_cs, float s_out = 1.f) {
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
   const int tiles_x = (Wo + kC0TW - 1) / kC0TW;
   const int tiles_y = (Ho + kC0TH - 1) / kC0TH;
@@ -1328,200 +1400,111 @@ __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ 
   bid /= tiles_x;
   const int ty = bid % tiles_y;
   const int b = bid / tiles_y;
-  const int oy0 = ty * kC0TH, ox0 = tx * kC0TW;
-  const int iy0 = oy0 * 2 - 1, bx0 = (ox0 * 2 - 1) * 3;  // first input row / byte column
-  const uint8_t* frame = img + (size_t)b * H * W * 3;
   const int tid = threadIdx.x;
-  // Stage the window as bf16 bit patterns, element e = byte column e - 1
-  // (so dword-aligned source words land on dword-aligned LDS pairs): all
-  // dword loads of a thread are issued before any conversion.
-  constexpr int kDw = (kC0IW + 1 + 3) / 4;             // dwords per row (388 B)
-  constexpr int kN = (2 * kC0TH + 1) * kDw;            // 1649
-  constexpr int kIt = (kN + 255) / 256;                // 7
-  const bool aligned_rows = (W * 3) % 4 == 0 && ((uintptr_t)frame & 3) == 0;
-  uint32_t dv[kIt];
+  const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
+  const int oy = ty * kC0TH + wave;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(img + (size_t)b * H * W * 3), 0, H * W * 3, kRsrcFlags);
+  C0Wts<MR> Wt;
+  Wt.load(q, 16 * MR, col, quad);
+  C0Win win[4];
 #pragma unroll
-  for (int it = 0; it < kIt; ++it) {
-    const int i = tid + it * 256;
-    dv[it] = 0;
-    if (i < kN) {
-      const int r = i / kDw, d = i - (i / kDw) * kDw;
-      const int iy = iy0 + r, a = bx0 - 1 + 4 * d;  // first byte of this word
-      if ((unsigned)iy < (unsigned)H) {
-        const uint8_t* row = frame + (size_t)iy * W * 3;
-        if (aligned_rows && a >= 0 && a + 3 < W * 3) {
-          dv[it] = *(const uint32_t*)(row + a);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (a + q >= 0 && a + q < W * 3) dv[it] |= (uint32_t)row[a + q] << (8 * q);
-        }
-      }
-    }
+  for (int j = 0; j < 4; ++j) {
+    const int ox = tx * kC0TW + 16 * j + col;
+    win[j] = conv0_window(r, oy, ox, quad, H, W * 3, oy < Ho && ox < Wo);
   }
 #pragma unroll
-  for (int it = 0; it < kIt; ++it) {
-    const int i = tid + it * 256;
-    if (i < kN) {
-      const int r = i / kDw, d = i - (i / kDw) * kDw;
-      // bf16 of a byte value v is the high half of the f32 (float)v
-      const uint32_t f0 = __float_as_uint((float)(dv[it] & 255));
-      const uint32_t f1 = __float_as_uint((float)((dv[it] >> 8) & 255));
-      const uint32_t f2 = __float_as_uint((float)((dv[it] >> 16) & 255));
-      const uint32_t f3 = __float_as_uint((float)(dv[it] >> 24));
-      uint32_t* dst = (uint32_t*)(xin + r * kC0RS + 4 * d);
-      dst[0] = (f0 >> 16) | (f1 & 0xFFFF0000u);
-      dst[1] = (f2 >> 16) | (f3 & 0xFFFF0000u);
-    }
-  }
-  const int wave = tid >> 6, lane = tid & 63;
-  const int col = lane & 15, quad = lane >> 4;
-  // A fragments: rows cout = 16m + col, k = 8*quad + j
-  bf16x8 Ah[MR], Am[MR], Al[MR];
-#pragma unroll
-  for (int m = 0; m < MR; ++m) {
-    const int co = 16 * m + col;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 8 * quad + j;
-      float v = 0.f;
-      if (k < 27) {
-        const int ky = k / 9, rem = k - ky * 9, kx = rem / 3, ch = rem - kx * 3;
-        v = w[((co * 3 + (2 - ch)) * 3 + ky) * 3 + kx] / 255.0f;
-      }
-      const __bf16 hi = (__bf16)v;
-      const float r1 = v - (float)hi;
-      const __bf16 mid = (__bf16)r1;
-      Ah[m][j] = hi;
-      Am[m][j] = mid;
-      Al[m][j] = (__bf16)(r1 - (float)mid);
-    }
-  }
-  float bv[MR][4];
-#pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bv[m][i] = bias[16 * m + 4 * quad + i];
-  // this lane's 8 k-value addresses for output pixel (row 0, x = 16*wave + col)
-  int koff[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 8 * quad + j;
-    const int kk = k < 27 ? k : 0;  // padded k: any value, its weight is 0
-    const int ky = kk / 9, rem = kk - ky * 9;
-    koff[j] = ky * kC0RS + (16 * wave + col) * 6 + rem + 1;  // element = byte column + 1
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < kC0TH; ++r) {
-    const int oy = oy0 + r;
-    bf16x8 X;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) X[j] = __builtin_bit_cast(__bf16, xin[koff[j] + 2 * r * kC0RS]);
-    f32x4 acc[MR];
+  for (int j = 0; j < 4; ++j) {
+    const int ox = tx * kC0TW + 16 * j + col;
+    f32x4 v[MR];
+    conv0_frag<MR>(Wt, conv0_bop(win[j]), v);
+    if (oy >= Ho || ox >= Wo) continue;
+    const size_t opix = (((size_t)b * Ho + oy) * Wo + ox) * out_cs;
 #pragma unroll
     for (int m = 0; m < MR; ++m) {
-      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al[m], X, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am[m], X, acc[m], 0, 0, 0);
-      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[m], X, acc[m], 0, 0, 0);
-    }
-    const int ox = ox0 + 16 * wave + col;
-    if (oy < Ho && ox < Wo) {
-      const size_t opix = (((size_t)b * Ho + oy) * Wo + ox) * out_cs;
-#pragma unroll
-      for (int m = 0; m < MR; ++m) {
-        const float v0 = silu(acc[m][0] + bv[m][0]), v1 = silu(acc[m][1] + bv[m][1]);
-        const float v2 = silu(acc[m][2] + bv[m][2]), v3 = silu(acc[m][3] + bv[m][3]);
-        if constexpr (F8) {
-          const float v[4] = {v0, v1, v2, v3};
-          *(uint32_t*)((uint8_t*)out + opix + 16 * m + 4 * quad) = f8_encode4(v, 1.0f / s_out);
-        } else {
-          *(uint2*)((uint16_t*)out + opix + 16 * m + 4 * quad) =
-              make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
-        }
+      if constexpr (F8) {
+        const float vv[4] = {v[m][0], v[m][1], v[m][2], v[m][3]};
+        *(uint32_t*)((uint8_t*)out + opix + 16 * m + 4 * quad) = f8_encode4(vv, 1.0f / s_out);
+      } else {
+        *(uint2*)((uint16_t*)out + opix + 16 * m + 4 * quad) =
+            make_uint2(pack_bf16x2(v[m][0], v[m][1]), pack_bf16x2(v[m][2], v[m][3]));
       }
     }
   }
 }
 
-int launch_conv0(const uint8_t* img, int B, int H, int W, const float* w, const float* bias,
-                 int C0, bf16_t* out, int out_cs, hipStream_t s) {
+template <bool F8>
+static int launch_conv0_t(const uint8_t* img, int B, int H, int W, const Conv0Q& q, int C0,
+                          void* out, int out_cs, float s_out, hipStream_t s) {
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
   const int blocks = B * ceil_div(Ho, kC0TH) * ceil_div(Wo, kC0TW);
-  if (C0 == 16) conv0_kernel<1><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
-  else if (C0 == 32) conv0_kernel<2><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
-  else if (C0 == 48) conv0_kernel<3><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
-  else if (C0 == 64) conv0_kernel<4><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
-  else if (C0 == 80) conv0_kernel<5><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs);
-  else {
-    set_error("conv0 C0=%d unsupported", C0);
-    return RV_EINVAL;
+  switch (C0) {
+    case 16: conv0_kernel<1, F8><<<blocks, 256, 0, s>>>(img, B, H, W, q, out, out_cs, s_out); break;
+    case 32: conv0_kernel<2, F8><<<blocks, 256, 0, s>>>(img, B, H, W, q, out, out_cs, s_out); break;
+    case 48: conv0_kernel<3, F8><<<blocks, 256, 0, s>>>(img, B, H, W, q, out, out_cs, s_out); break;
+    case 64: conv0_kernel<4, F8><<<blocks, 256, 0, s>>>(img, B, H, W, q, out, out_cs, s_out); break;
+    case 80: conv0_kernel<5, F8><<<blocks, 256, 0, s>>>(img, B, H, W, q, out, out_cs, s_out); break;
+    default:
+      set_error("conv0 C0=%d unsupported", C0);
+      return RV_EINVAL;
   }
-  return launch_status("conv0");
+  return launch_status(F8 ? "conv0_fp8" : "conv0");
 }
 
-int launch_conv0_fp8(const uint8_t* img, int B, int H, int W, const float* w, const float* bias,
-                     int C0, uint8_t* out, int out_cs, float s_out, hipStream_t s) {
-  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
-  const int blocks = B * ceil_div(Ho, kC0TH) * ceil_div(Wo, kC0TW);
-  if (C0 == 16) conv0_kernel<1, true><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs, s_out);
-  else if (C0 == 32) conv0_kernel<2, true><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs, s_out);
-  else if (C0 == 48) conv0_kernel<3, true><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs, s_out);
-  else if (C0 == 64) conv0_kernel<4, true><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs, s_out);
-  else if (C0 == 80) conv0_kernel<5, true><<<blocks, 256, 0, s>>>(img, B, H, W, w, bias, out, out_cs, s_out);
-  else {
-    set_error("conv0 C0=%d unsupported", C0);
-    return RV_EINVAL;
-  }
-  return launch_status("conv0_fp8");
+int launch_conv0(const uint8_t* img, int B, int H, int W, const Conv0Q& q, int C0, bf16_t* out,
+                 int out_cs, hipStream_t s) {
+  return launch_conv0_t<false>(img, B, H, W, q, C0, out, out_cs, 1.f, s);
+}
+
+int launch_conv0_fp8(const uint8_t* img, int B, int H, int W, const Conv0Q& q, int C0,
+                     uint8_t* out, int out_cs, float s_out, hipStream_t s) {
+  return launch_conv0_t<true>(img, B, H, W, q, C0, out, out_cs, s_out, s);
 }
 
 // ---------------------------------------------------------------------------
-// Fused stem: conv0 (3 -> C0, k3 s2, from the u8 letterbox) and model.1
-// (C0 -> C1, k3 s2) in one kernel; the C0-channel P1 map (X0) only ever
-// lives in LDS.  X0 is the largest activation of the network (B x 192 x 320 x
-// 16 bf16 at 1080p) and model.1 would otherwise read it back with a 3x3
-// halo; here each workgroup computes the X0 pixels its X1 tile needs
-// (halo recomputed, ~13 %) and convolves them straight from LDS.
+// Fused stem: conv0 (3 -> C0 = 16, k3 s2, from the u8 letterbox), model.1
+// (16 -> 32, k3 s2) and model.2.cv1 (32 -> 32 1x1) in one kernel.  The P1
+// map (X0, the network's largest activation) only ever lives in LDS: each
+// workgroup computes the X0 pixels its X1 tile needs (halo recomputed,
+// 8 %) with the conv0 fragments above (window bytes straight from L2; no
+// letterbox staging), then convolves them from LDS.
 //
-// model.1 with C0 = 16 input channels runs on "tap pairs": a 32-deep MFMA
-// k-step takes 16 channels of two horizontally adjacent taps (kx, kx+1),
-// which are two adjacent X0 pixels -- 64 contiguous bytes of the 32-B-per-
-// pixel LDS image -- so a row of taps is 2 k-steps instead of 3 zero-padded
-// ones (the phantom 4th tap has zero weights).  A fragments come straight
-// from the standard packed weights [Cout][ky][kx][32] (L2-resident).
+// X0 tile in LDS: 17 rows x (33 even + 32 odd columns) of 32-B pixels, the
+// even tile columns first, then the odd ones (stored column of tile column
+// xr: xr / 2, or 33 + xr / 2).  model.1 runs on "tap pairs": a 32-deep MFMA
+// k-step takes the 16 channels of two taps -- (kx 0, kx 1) = (even c, odd
+// c) for X1 column c, then (kx 2, phantom) = even c + 1 with zero weights
+// for the phantom -- so 16 consecutive X1 pixels read 16 consecutive 32-B
+// stored pixels of one region: every ds_read_b128 lane group hits 16
+// distinct 16-B bank slots (the interleaved image this replaces was 2-way
+// conflicted).  A fragments come from the standard packed weights
+// [Cout][ky][kx][32] and are held in registers for the whole kernel.
 //
-// Tile: 8 x 32 X1 pixels x 32 couts per workgroup; wave w owns X1 rows 2w,
-// 2w+1 (4 fragments of 16 pixels).  X0 tile: 17 x 66 pixels (the 66th column
-// only feeds the phantom tap).  Letterbox tile: 35 rows x 133 pixels as bf16
-// bit patterns.
-constexpr int kStR = 8, kStC = 32;                      // X1 tile
-constexpr int kStXR = 2 * kStR + 1, kStXC = 2 * kStC + 2;  // X0 tile (17 x 66)
-constexpr int kStLR = 2 * kStXR + 1, kStLC = 2 * kStXC + 1;  // lb tile (35 x 133 px)
-constexpr int kStLS = kStLC * 3 + 5;                    // lb row stride (bytes), 404
-constexpr int kStXB = kStXR * kStXC * 32;               // X0 tile bytes (35,904)
-constexpr int kStLB = kStLR * kStLS;                    // lb tile bytes (14,140)
+// With model.2.cv1 fused, model.1's output channels are computed in the
+// order that leaves lane quad q holding channels 8q .. 8q+7 of its pixel
+// (fragment m, row 4q'+i = channel 8q' + 4m + i): exactly the B operand of
+// a K = 32 MFMA in natural k order, so cv1 runs straight from the registers
+// with the operands (and k order) of the unfused 1x1 kernels --
+// bit-identical -- and X1 never reaches HBM (out == nullptr; out !=
+// nullptr still writes it, for parity tests).
+constexpr int kStR = 8, kStC = 32;           // X1 tile
+constexpr int kStXR = 2 * kStR + 1;          // X0 tile rows (17)
+constexpr int kStXE = kStC + 1;              // even X0 tile columns (33)
+constexpr int kStXW = 2 * kStC + 1;          // stored pixels per row (33 even + 32 odd)
+constexpr int kStRowB = kStXW * 32;          // 2080 B per X0 tile row
+constexpr int kStXB = kStXR * kStRowB;       // 35,360 B
+constexpr int kStNpx = kStXR * kStXW;        // 1105 X0 pixels per tile
+constexpr int kStNfr = (kStNpx + 15) / 16;   // 70 conv0 fragments
 
-//
-// With the next 1x1 conv fused (cv1: 32 -> 32, model.2.cv1 of YOLOv8n), the
-// model.1 output channels are computed in the order that leaves lane quad q
-// holding channels 8q .. 8q+7 of its pixel (fragment m, row 4q'+i = channel
-// 8q' + 4m + i): exactly the B operand of a K = 32 MFMA in natural k order,
-// so cv1 runs straight from the registers with the operands (and k order)
-// of the unfused 1x1 kernels -- bit-identical -- and X1 never reaches HBM
-// (out == nullptr; out != nullptr still writes it, for parity tests).
 __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ img, int B, int H,
-                                                   int W, const float* __restrict__ w0,
-                                                   const float* __restrict__ b0,
+                                                   int W, Conv0Q q0,
                                                    const uint16_t* __restrict__ w1,
                                                    const float* __restrict__ b1,
                                                    uint16_t* __restrict__ out, int out_cs,
                                                    const uint16_t* __restrict__ w2,
                                                    const float* __restrict__ b2,
                                                    uint16_t* __restrict__ out2, int out2_cs) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* xs = smem;                               // X0 tile: [17][66] px x 32 B
-  uint8_t* ls = smem + kStXB;                       // lb tile: [35][404] u8
+  __shared__ __attribute__((aligned(16))) uint8_t xs[kStXB];
   const int H0 = (H + 1) / 2, W0 = (W + 1) / 2;     // X0 map
   const int H1 = (H0 + 1) / 2, W1 = (W0 + 1) / 2;   // X1 map
   const int tiles_x = (W1 + kStC - 1) / kStC, tiles_y = (H1 + kStR - 1) / kStR;
@@ -1532,142 +1515,92 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
   const int b = bid / tiles_y;
   const int oy0 = ty * kStR, ox0 = tx * kStC;        // X1 tile origin
   const int xy0 = 2 * oy0 - 1, xx0 = 2 * ox0 - 1;    // X0 tile origin
-  const int ly0 = 2 * xy0 - 1, lx0 = 2 * xx0 - 1;    // lb tile origin (pixels)
-  const uint8_t* frame = img + (size_t)b * H * W * 3;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(img + (size_t)b * H * W * 3), 0, H * W * 3, kRsrcFlags);
 
-  // ---- 1. letterbox tile -> LDS as u8 (0 outside the image); the bf16 bit
-  //      patterns of the (exact) byte values are formed when gathered
+  // ---- 1. conv0 over the X0 tile, fragment f = stored pixels 16 f .. +15
   {
-    constexpr int kDw = (kStLC * 3 + 1 + 3) / 4;       // dwords per row (covers 399 B + 1)
-    constexpr int kN = kStLR * kDw;
-    const int bx0 = lx0 * 3;
-    const bool aligned_rows = (W * 3) % 4 == 0 && ((uintptr_t)frame & 3) == 0;
-    for (int i0 = tid; i0 < kN; i0 += 4 * 256) {
-      uint32_t dv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = i0 + u * 256;
-        dv[u] = 0;
-        if (i < kN) {
-          const int r = i / kDw, d = i - (i / kDw) * kDw;
-          const int iy = ly0 + r, a = bx0 - 1 + 4 * d;  // first byte of this word
-          if ((unsigned)iy < (unsigned)H) {
-            const uint8_t* row = frame + (size_t)iy * W * 3;
-            if (aligned_rows && a >= 0 && a + 3 < W * 3) {
-              dv[u] = *(const uint32_t*)(row + a);
-            } else {
-#pragma unroll
-              for (int q = 0; q < 4; ++q)
-                if (a + q >= 0 && a + q < W * 3) dv[u] |= (uint32_t)row[a + q] << (8 * q);
-            }
-          }
-        }
+    C0Wts<1> Wt;
+    Wt.load(q0, 16, col, quad);
+    auto pix = [&](int f, int& Y, int& X, bool& ok) {
+      const int s = f * 16 + col;
+      const int yr = s / kStXW, j = s - (s / kStXW) * kStXW;
+      const int xr = j < kStXE ? 2 * j : 2 * (j - kStXE) + 1;
+      Y = xy0 + yr;
+      X = xx0 + xr;
+      ok = s < kStNpx && (unsigned)Y < (unsigned)H0 && (unsigned)X < (unsigned)W0;
+    };
+    int Y, X;
+    bool ok;
+    pix(wave, Y, X, ok);
+    C0Win nxt = conv0_window(r, Y, X, quad, H, W * 3, ok);
+    for (int f = wave; f < kStNfr; f += 4) {
+      const C0Win cur = nxt;
+      const bool cok = ok;
+      if (f + 4 < kStNfr) {
+        pix(f + 4, Y, X, ok);
+        nxt = conv0_window(r, Y, X, quad, H, W * 3, ok);
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = i0 + u * 256;
-        if (i < kN) {
-          const int r = i / kDw, d = i - (i / kDw) * kDw;
-          *(uint32_t*)(ls + r * kStLS + 4 * d) = dv[u];  // element e = byte column e - 1
-        }
-      }
+      f32x4 v[1];
+      conv0_frag<1>(Wt, conv0_bop(cur), v);
+      // outside the X0 map the value is model.1's zero padding
+      const uint2 pk = cok ? make_uint2(pack_bf16x2(v[0][0], v[0][1]), pack_bf16x2(v[0][2], v[0][3]))
+                           : make_uint2(0, 0);
+      const int s = f * 16 + col;
+      if (s < kStNpx) *(uint2*)(xs + s * 32 + quad * 8) = pk;
     }
   }
-  // conv0 weights: A rows cout = col, k = 8*quad + j over (ky, kx, ch) with
-  // BGR -> RGB and 1/255 folded in, split hi + mid + lo bf16 (as conv0_kernel)
-  bf16x8 Ah, Am, Al;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 8 * quad + j;
-    float v = 0.f;
-    if (k < 27) {
-      const int ky = k / 9, rem = k - ky * 9, kx = rem / 3, ch = rem - kx * 3;
-      v = w0[((col * 3 + (2 - ch)) * 3 + ky) * 3 + kx] / 255.0f;
-    }
-    const __bf16 hi = (__bf16)v;
-    const float r1 = v - (float)hi;
-    const __bf16 mid = (__bf16)r1;
-    Ah[j] = hi;
-    Am[j] = mid;
-    Al[j] = (__bf16)(r1 - (float)mid);
-  }
-  float bias0[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) bias0[i] = b0[4 * quad + i];
-  int koff[8];  // lb tile element offsets of this lane's 8 k values (pixel 0, 0)
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 8 * quad + j;
-    const int kk = k < 27 ? k : 0;  // padded k: any value, its weight is 0
-    const int ky = kk / 9, rem = kk - ky * 9;
-    koff[j] = ky * kStLS + rem + 1;  // element = byte column + 1
-  }
-  __syncthreads();
-
-  // ---- 2. conv0 for the X0 tile (17 x 66 pixels, 16-pixel fragments)
-  constexpr int kXpx = kStXR * kStXC;                // 1122
-  constexpr int kXfr = (kXpx + 15) / 16;             // 71
-  for (int f = wave; f < kXfr; f += 4) {
-    const int i = f * 16 + col;                      // X0 tile pixel of this lane (B column)
-    const int ii = i < kXpx ? i : 0;
-    const int yr = ii / kStXC, xr = ii - (ii / kStXC) * kStXC;
-    const int base = 2 * yr * kStLS + 2 * xr * 3;
-    bf16x8 X;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      X[j] = __builtin_bit_cast(__bf16, (uint16_t)(__float_as_uint((float)ls[base + koff[j]]) >> 16));
-    f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, X, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, X, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, X, acc, 0, 0, 0);
-    // lane holds couts 4*quad .. 4*quad+3 of pixel i; outside the X0 map the
-    // value is model.1's zero padding
-    const int gy = xy0 + yr, gx = xx0 + xr;
-    const bool inside = i < kXpx && (unsigned)gy < (unsigned)H0 && (unsigned)gx < (unsigned)W0;
-    uint2 pk = make_uint2(0, 0);
-    if (inside)
-      pk = make_uint2(pack_bf16x2(silu(acc[0] + bias0[0]), silu(acc[1] + bias0[1])),
-                      pack_bf16x2(silu(acc[2] + bias0[2]), silu(acc[3] + bias0[3])));
-    if (i < kXpx) *(uint2*)(xs + i * 32 + quad * 8) = pk;
-  }
-  __syncthreads();
-
-  // ---- 3. model.1 (C0 = 16 -> 32, k3 s2) on tap pairs from the X0 tile
+  // model.1 A fragments (all 6 k-steps, L2-resident weights) while the
+  // conv0 stores drain
   constexpr int MR = 2, NR = 4;
-  f32x4 acc[MR][NR];
-#pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // this lane's B column: X1 pixel (row 2*wave + n/2, col (n&1)*16 + col)
-  int bbase[NR];
-#pragma unroll
-  for (int n = 0; n < NR; ++n) {
-    const int r = 2 * wave + (n >> 1), c = (n & 1) * 16 + col;
-    bbase[n] = ((2 * r) * kStXC + 2 * c) * 32 + quad * 16;
-  }
+  bf16x8 A[3][2][MR];
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-      bf16x8 A[MR], Bf[NR];
       const int kx = 2 * p + (quad >> 1);  // quads 0,1: tap 2p; quads 2,3: tap 2p+1
 #pragma unroll
       for (int m = 0; m < MR; ++m) {
         const int co = 8 * (col >> 2) + 4 * m + (col & 3);  // row col of fragment m
         uint4 v = make_uint4(0, 0, 0, 0);
         if (kx < 3) v = *(const uint4*)(w1 + ((size_t)co * 9 + ky * 3 + kx) * 32 + (quad & 1) * 8);
-        A[m] = __builtin_bit_cast(bf16x8, v);
+        A[ky][p][m] = __builtin_bit_cast(bf16x8, v);
       }
+    }
+  __syncthreads();
+
+  // ---- 2. model.1 (C0 = 16 -> 32, k3 s2) on tap pairs from the X0 tile
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // this lane's B column: X1 pixel (row 2 wave + n / 2, col (n & 1) 16 + col)
+  int bb0[NR], bb1[NR];
+#pragma unroll
+  for (int n = 0; n < NR; ++n) {
+    const int rr = 2 * wave + (n >> 1), c = (n & 1) * 16 + col;
+    const int rb = 2 * rr * kStRowB;
+    // pair 0: quads 0,1 tap kx 0 (even c), quads 2,3 tap kx 1 (odd c)
+    bb0[n] = rb + (quad < 2 ? c * 32 + quad * 16 : (kStXE + c) * 32 + (quad - 2) * 16);
+    // pair 1: tap kx 2 (even c + 1); quads 2,3 (phantom tap) read the same
+    bb1[n] = rb + (c + 1) * 32 + (quad & 1) * 16;
+  }
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      bf16x8 Bf[NR];
 #pragma unroll
       for (int n = 0; n < NR; ++n)
-        Bf[n] = __builtin_bit_cast(bf16x8, *(const uint4*)(xs + bbase[n] + (ky * kStXC + 2 * p) * 32));
+        Bf[n] = __builtin_bit_cast(bf16x8, *(const uint4*)(xs + (p ? bb1[n] : bb0[n]) + ky * kStRowB));
 #pragma unroll
       for (int m = 0; m < MR; ++m)
 #pragma unroll
         for (int n = 0; n < NR; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[m], Bf[n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ky][p][m], Bf[n], acc[m][n], 0, 0, 0);
     }
   // epilogue: bias + SiLU -> X1 values (bf16); lane quad q of fragment m
   // holds channels 8q + 4m .. 8q + 4m + 3
@@ -1720,7 +1653,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
   }
 }
 
-int launch_stem(const uint8_t* img, int B, int H, int W, const float* w0, const float* b0, int C0,
+int launch_stem(const uint8_t* img, int B, int H, int W, const Conv0Q& q0, int C0,
                 const bf16_t* w1, const float* b1, int C1, bf16_t* out, int out_cs,
                 hipStream_t s, const bf16_t* w2, const float* b2, bf16_t* out2, int out2_cs) {
   if (C0 != 16 || C1 != 32 || (!out && !out2) || (out2 && (!w2 || !b2))) {
@@ -1730,18 +1663,8 @@ int launch_stem(const uint8_t* img, int B, int H, int W, const float* w0, const 
   const int H0 = (H + 1) / 2, W0 = (W + 1) / 2;
   const int H1 = (H0 + 1) / 2, W1 = (W0 + 1) / 2;
   const int blocks = B * ceil_div(H1, kStR) * ceil_div(W1, kStC);
-  const size_t smem = (size_t)kStXB + kStLB;
-  static bool attr = false;
-  if (!attr) {
-    // best effort: a failure surfaces as the launch error reported below
-    (void)hipFuncSetAttribute((const void*)stem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    (void)hipGetLastError();
-    attr = true;
-  }
-  stem_kernel<<<blocks, 256, smem, s>>>(img, B, H, W, w0, b0, (const uint16_t*)w1, b1,
-                                        (uint16_t*)out, out_cs, (const uint16_t*)w2, b2,
-                                        (uint16_t*)out2, out2_cs);
+  stem_kernel<<<blocks, 256, 0, s>>>(img, B, H, W, q0, (const uint16_t*)w1, b1, (uint16_t*)out,
+                                     out_cs, (const uint16_t*)w2, b2, (uint16_t*)out2, out2_cs);
   return launch_status("stem");
 }
 

@@ -65,6 +65,10 @@ struct ModelDef {
   Variant v;
   int dtype = 0;  // RV_YOLO_DTYPE_BF16 / RV_YOLO_DTYPE_FP8
   std::vector<ConvSpec> convs;
+  // conv 0's integer form (the i8 MFMA conv0, conv.h Conv0Q), after every
+  // conv's block: digits [3][C0][64] i8, scales [C0] f32, biases [C0] f32,
+  // accumulator starts [3][C0] i32
+  size_t q_off = 0, q_bytes = 0;
   int add(const std::string& n, int ci, int co, int k, int s, int act = 1) {
     ConvSpec c;
     c.name = n;
@@ -91,6 +95,8 @@ struct ModelDef {
     return -1;
   }
 };
+
+static size_t conv0q_bytes(int C0) { return 3 * (size_t)C0 * 64 + 20 * (size_t)C0; }
 
 static bool build_def(int variant, ModelDef& m, int dtype = RV_YOLO_DTYPE_BF16) {
   if (!variant_widths(variant, m.v)) return false;
@@ -151,13 +157,57 @@ static bool build_def(int variant, ModelDef& m, int dtype = RV_YOLO_DTYPE_BF16) 
       off = al(off + (size_t)cop * 4);
     }
   }
+  m.q_off = off;
+  m.q_bytes = conv0q_bytes(m.convs[0].cout);
   return true;
 }
 
 static size_t packed_bytes(const ModelDef& m) {
-  const ConvSpec& c = m.convs.back();
-  const size_t last = c.f8 ? c.ws_off : c.b_off;
-  return ((last + (size_t)((c.cout + 15) & ~15) * 4) + 255) & ~(size_t)255;
+  return (m.q_off + m.q_bytes + 255) & ~(size_t)255;
+}
+
+// Integer form of conv 0 (conv.h Conv0Q): per output channel o, the f64
+// weights V[k] = w[o][2-ch][ky][kx] / 255 (RGB order and 1/255 folded in;
+// k = 16 ky + 3 kx + ch over the window's BGR bytes, k % 16 >= 9 zero) as
+// integers Q[k] = round(V[k] / s), s = max|V| / (127 * 2^16), split into
+// balanced base-256 digits Q = 65536 D0 + 256 D1 + D2 (each in [-128, 127]).
+// The kernel feeds x - 128 (the byte XOR 0x80) to one i8 MFMA per digit,
+// starting each accumulator at 128 sum_k D_i[k], so it holds T_i = sum_k
+// D_i[k] x[k] exactly (|T_i| <= 27 * 128 * 255 < 2^24: exact in f32 too);
+// the value is s (65536 T0 + 256 T1 + T2) + b, f32 to 2^-23 of the weight
+// scale with no offset cancellation.
+static void pack_conv0q(const float* w, const float* b, int C0, uint8_t* dst) {
+  int8_t* D = (int8_t*)dst;
+  float* S = (float*)(dst + 3 * (size_t)C0 * 64);
+  float* Bv = S + C0;
+  int32_t* Cq = (int32_t*)(Bv + C0);
+  for (int o = 0; o < C0; ++o) {
+    double V[64] = {0.0}, M = 0.0;
+    for (int ky = 0; ky < 3; ++ky)
+      for (int kx = 0; kx < 3; ++kx)
+        for (int ch = 0; ch < 3; ++ch) {
+          const double v = (double)w[((o * 3 + (2 - ch)) * 3 + ky) * 3 + kx] / 255.0;
+          V[16 * ky + 3 * kx + ch] = v;
+          M = std::max(M, std::fabs(v));
+        }
+    const float s = M > 0.0 ? (float)(M / (127.0 * 65536.0)) : 1.0f;
+    long long sd[3] = {0, 0, 0};
+    for (int k = 0; k < 64; ++k) {
+      const long long q = std::llround(V[k] / (double)s);
+      const long long d2 = ((q + 128) & 255) - 128;
+      const long long q1 = (q - d2) / 256;
+      const long long d1 = ((q1 + 128) & 255) - 128;
+      const long long d0 = (q1 - d1) / 256;
+      const long long d[3] = {d0, d1, d2};
+      for (int t = 0; t < 3; ++t) {
+        D[((size_t)t * C0 + o) * 64 + k] = (int8_t)d[t];
+        sd[t] += d[t];
+      }
+    }
+    S[o] = s;
+    Bv[o] = b[o];
+    for (int t = 0; t < 3; ++t) Cq[t * C0 + o] = (int32_t)(128 * sd[t]);
+  }
 }
 
 static size_t flat_floats(const ModelDef& m) {
@@ -719,6 +769,7 @@ extern "C" int rv_yolo_pack2(int variant, int dtype, const float* flat, size_t n
     p += nw + c.cout;
     if (i == 0) {
       memcpy(out + c.w_off, w, nw * 4);
+      pack_conv0q(w, b, c.cout, out + m.q_off);
     } else if (c.f8) {
       // per output channel: scale = 2^ceil(log2(amax / 448)), codes RNE
       const int cip = (c.cin + 63) & ~63;
@@ -921,6 +972,9 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
   if (part != 2) {
   // backbone
   const ConvSpec& c0 = M->def.convs[0];
+  const uint8_t* qb = M->dev + M->def.q_off;
+  const float* qs = (const float*)(qb + 3 * (size_t)c0.cout * 64);
+  const Conv0Q q0{(const int8_t*)qb, qs, qs + c0.cout, (const int32_t*)(qs + 2 * c0.cout)};
   // conv0 + model.1 fused (the P1 map stays in LDS) unless the caller asked
   // for the raw prediction with RV_YOLO_OPT_RAW_UNFUSED set (layer parity
   // forwards keep every activation in the workspace) or RV_FUSE_STEM=0
@@ -943,19 +997,43 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
     if (cv)
       E.trace(i2cv1, E.args(*cv, View{M->X1, v.c2, 0}, 2, View{M->C2, c2cs, 0}, 0, none, 0, none),
               View{M->X1, v.c2, 0}, View{M->C2, c2cs, 0}, 0, none, 0, none);
-    st = launch_stem(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
-                     (const float*)(M->dev + c0.b_off), c0.cout, E.wptr(c1), E.bptr(c1), c1.cout,
-                     (!cv || M->stem_x1) ? (bf16_t*)E.ptr(M->X1) : nullptr, v.c2, E.s,
-                     cv ? E.wptr(*cv) : nullptr, cv ? E.bptr(*cv) : nullptr,
-                     cv ? (bf16_t*)E.ptr(M->C2) : nullptr, c2cs);
-    if (st) return st;
+    // the stem is timed with the conv launches (profile slot per_fwd - 1,
+    // which no conv launch index reaches: a forward has fewer launches than
+    // convs)
+    Profile& P = M->prof;
+    const int slot = P.per_fwd - 1;
+    const bool rec = P.on && P.n_fwd < P.cap_fwd && slot >= 0;
+    const bool x1_out = !cv || M->stem_x1;
+    if (rec) {
+      const double px0 = (double)B * M->map_h[1] * M->map_w[1];
+      const double px1 = (double)B * M->map_h[2] * M->map_w[2];
+      P.flops[slot] = 2.0 * px0 * c0.cout * 27 + 2.0 * px1 * c1.cout * c1.cin * 9 +
+                      (cv ? 2.0 * px1 * cv->cout * cv->cin : 0.0);
+      // letterbox read once, X1 / the cv1 slice written once, weights once
+      P.bytes[slot] = (double)B * M->H * M->W * 3 + px1 * 2.0 * (x1_out ? c1.cout : 0) +
+                      (cv ? px1 * 2.0 * cv->cout : 0.0) + M->def.q_bytes + 2.0 * c1.cout * 9 * 32 +
+                      (cv ? 2.0 * cv->cout * 32 : 0.0);
+      P.conv_of[slot] = 0;
+      st = hip_check(hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + slot) * 2], E.s),
+                     "profile hipEventRecord");
+      if (st) return st;
+    }
+    for (int r = 0; r < (rec ? P.reps : 1); ++r) {
+      st = launch_stem(lb, B, M->H, M->W, q0, c0.cout, E.wptr(c1), E.bptr(c1), c1.cout,
+                       x1_out ? (bf16_t*)E.ptr(M->X1) : nullptr, v.c2, E.s,
+                       cv ? E.wptr(*cv) : nullptr, cv ? E.bptr(*cv) : nullptr,
+                       cv ? (bf16_t*)E.ptr(M->C2) : nullptr, c2cs);
+      if (st) return st;
+    }
+    if (rec) {
+      st = hip_check(hipEventRecord(P.ev[((size_t)P.n_fwd * P.per_fwd + slot) * 2 + 1], E.s),
+                     "profile hipEventRecord");
+      if (st) return st;
+    }
   } else {
-    st = f8 ? launch_conv0_fp8(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
-                               (const float*)(M->dev + c0.b_off), c0.cout, (uint8_t*)E.ptr(M->X0),
-                               v.c1, E.scale(M->X0), E.s)
-            : launch_conv0(lb, B, M->H, M->W, (const float*)(M->dev + c0.w_off),
-                           (const float*)(M->dev + c0.b_off), c0.cout, (bf16_t*)E.ptr(M->X0), v.c1,
-                           E.s);
+    st = f8 ? launch_conv0_fp8(lb, B, M->H, M->W, q0, c0.cout, (uint8_t*)E.ptr(M->X0), v.c1,
+                               E.scale(M->X0), E.s)
+            : launch_conv0(lb, B, M->H, M->W, q0, c0.cout, (bf16_t*)E.ptr(M->X0), v.c1, E.s);
     if (st) return st;
     E.conv("model.1", View{M->X0, v.c1, 0}, 1, View{M->X1, v.c2, 0});
   }

@@ -84,7 +84,10 @@ def _layout(variant):
             ws_off = off
             off = al(off + cop * 4)
         out.append((n, ci, co, k, f8, cip, w_off, b_off, ws_off))
-    return out, off
+    # conv 0's integer form (pack_conv0q) closes the blob: digits [3][C0][64]
+    # i8, scales [C0] f32, biases [C0] f32, accumulator starts [3][C0] i32
+    c0 = specs[0][2]
+    return out, al(off + 3 * c0 * 64 + 20 * c0)
 
 
 def test_fp8_packer_matches_oracle_quantiser():

@@ -1,5 +1,5 @@
 """HBM traffic of the conv launches (conv_patch_kernel + conv1x1_direct_kernel +
-c2f_chain_kernel)
+c2f_chain_kernel + stem_kernel)
 of one bench step from the PMC
 passes of tools/gpu_pmc.sh (FETCH_SIZE / WRITE_SIZE, KB): per the gfx950
 calibration in MI355X_MICROARCH.md, FETCH_SIZE counts half the bytes of a
@@ -14,7 +14,7 @@ import sys
 sys.path[:0] = [os.path.dirname(os.path.abspath(__file__))]
 from pmc_report import load  # noqa: E402
 
-CONV_KERNELS = ("conv_patch_kernel", "conv1x1_direct_kernel", "c2f_chain_kernel")
+CONV_KERNELS = ("conv_patch_kernel", "conv1x1_direct_kernel", "c2f_chain_kernel", "stem_kernel")
 
 
 def main():

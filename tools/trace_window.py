@@ -14,7 +14,7 @@ import csv
 import sys
 from collections import defaultdict
 
-CONV = ("conv_patch_kernel", "conv1x1_direct_kernel", "c2f_chain_kernel")
+CONV = ("conv_patch_kernel", "conv1x1_direct_kernel", "c2f_chain_kernel", "stem_kernel")
 
 
 def family(name: str) -> str:
