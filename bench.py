@@ -83,6 +83,11 @@ def parse_args(argv=None):
     ap.add_argument("--pair", type=int, default=int(os.environ.get("RV_PAIR", 4)),
                     help="steps per pipeline unit (one forward over pair x streams frames); the "
                          "largest divisor of --steps not above it is used")
+    ap.add_argument("--units", default=os.environ.get("RV_UNITS", "even"),
+                    help="pipeline unit sizes: 'even' (--steps / pair units of pair steps), "
+                         "'ramp' (units of 1 and 2 steps at both ends of the run, pair steps "
+                         "between: a shorter pipeline fill and drain), or an explicit "
+                         "comma-separated list summing to --steps")
     ap.add_argument("--warm-runs", type=int, default=int(os.environ.get("RV_WARM_RUNS", 1)),
                     help="untimed runs of the recorded schedule over the timed frames before the "
                          "timed region (warm-up of the schedule itself)")
@@ -119,6 +124,32 @@ def pick_pair(steps: int, pair: int) -> int:
     return max(p for p in range(1, max(1, pair) + 1) if steps % p == 0)
 
 
+def unit_sizes(steps: int, pair: int, spec: str) -> list:
+    """Steps per pipeline unit, in order (rvs_amd.schedule.PipelinedRun
+    units).  'even': steps / p units of p = pick_pair(steps, pair); 'ramp':
+    1- and 2-step units at both ends (the first unit's preprocess and the
+    last unit's forward + tracking run with little beside them, so small end
+    units shorten the fill and the drain), units of `pair` between, any
+    remainder as one unit in the middle; else an explicit list."""
+    if spec == "even":
+        p = pick_pair(steps, pair)
+        return [p] * (steps // p)
+    if spec == "ramp":
+        head = [h for h in (1, 2) if h < pair]
+        if 2 * sum(head) + pair > steps:
+            p = pick_pair(steps, pair)
+            return [p] * (steps // p)
+        mid = steps - 2 * sum(head)
+        body = [pair] * (mid // pair)
+        if mid % pair:
+            body.insert(len(body) // 2, mid % pair)
+        return head + body + head[::-1]
+    units = [int(x) for x in spec.split(",") if x.strip()]
+    if sum(units) != steps or min(units) < 1:
+        raise SystemExit(f"--units {spec}: sizes must be >= 1 and sum to --steps {steps}")
+    return units
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -152,7 +183,8 @@ class BenchJob:
         self.cfg = bench_config()
         self.S, self.K, self.Wm = args.streams, args.steps, args.warmup
         seq = args.exec_mode == "sequential"
-        lanes, pair = (1, 1) if seq else (2, pick_pair(args.steps, args.pair))
+        self.unit_sizes = None if seq else unit_sizes(args.steps, args.pair, args.units)
+        lanes, pair = (1, 1) if seq else (2, max(self.unit_sizes))
         self.eng = RoadVisionEngine(self.cfg, self.S, (H, W), device=dev, tmax=args.tmax,
                                     lanes=lanes, pair=pair)
         self.frames = road_frames(self.S, self.Wm + self.K, H, W, device=dev,
@@ -203,7 +235,7 @@ class BenchJob:
             from rvs_amd.schedule import PipelinedRun
             self.runner = PipelinedRun(eng, [self.frames[Wm + k] for k in range(K)],
                                        [self.ts[Wm + k] for k in range(K)], mode=a.exec_mode,
-                                       sync=a.sync)
+                                       sync=a.sync, units=self.unit_sizes)
             self.records = self.runner.records
             if a.warm_runs > 0:
                 # the SORT state is restored afterwards, so the timed run sees
@@ -303,7 +335,8 @@ def _conv_pass(job, mode: str, tags):
     _lib.call("rv_trace_marker", tags[0], st)
     if mode == "overlap":  # the timed region's schedule, issued eagerly with the events
         prof = PipelinedRun(eng, [job.frames[Wm + k] for k in range(K)],
-                            [job.ts[Wm + k] for k in range(K)], mode="eager", sync=job.args.sync)
+                            [job.ts[Wm + k] for k in range(K)], mode="eager", sync=job.args.sync,
+                            units=job.unit_sizes)
         prof.run()
     elif eng.pair > 1:  # each launch alone, on the timed region's forward batch
         from rvs_amd.handback import Record
@@ -583,7 +616,7 @@ def main(argv=None):
     P = job.eng.pair
     execution = ("sequential step() calls (no pipelining)" if args.exec_mode == "sequential" else
                  f"{args.exec_mode} launch list (rvs_amd.schedule.PipelinedRun, sync={args.sync}):"
-                 f" 4-stage software pipeline over units of {P} steps -- second half of unit "
+                 f" 4-stage software pipeline over units of {job.unit_sizes} steps -- second half of unit "
                  "u-1's forward || preprocess of unit u+1 || first half of unit u's forward || "
                  "NMS+SORT+hand-back of unit u-2 -- on 4 HIP streams, one C call per run")
     res = {

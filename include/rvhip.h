@@ -229,9 +229,12 @@ int rv_yolo_forward_part(void* handle, const uint8_t* lb, int B, void* ws, size_
 
 /* Introspection for layer-wise parity tests: activation buffers (NHWC,
  * info = {H, W, C, is_f32}, byte offset inside the workspace for batch B)
- * and the conv launches of the last forward (20 ints each: conv index,
+ * and the conv launches of the last forward (24 ints each: conv index,
  * input view {buf, cs, co, Hin, Win}, Ho, Wo, two output views {buf, cs, co,
- * upsample}, residual view {buf, cs, co}, pad).  Returns the record count. */
+ * upsample}, residual view {buf, cs, co}, then a 1x1 conv's virtual concat
+ * input {in_up, in2 buf, in2 cs, in2 co, split}: channels [0, split) are the
+ * input view's (read upsampled 2x when in_up), the rest in2's; in2 buf -1:
+ * none).  Returns the record count. */
 int rv_yolo_num_buffers(void* handle);
 int rv_yolo_buffer_info(void* handle, int B, int buf, int* info, size_t* off_bytes);
 int rv_yolo_trace(void* handle, int* recs, int max_recs);

@@ -50,6 +50,14 @@ struct ConvArgs {
   float s_in, s_res, s_out0, s_out1;
   const float* wscale;
   const float* g2_wscale;
+  // virtual concat input of a 1x1 conv (conv1x1_direct_kernel only): input
+  // channels [0, split) come from the `in` view -- read at (y/2, x/2) of a
+  // half-resolution map when in_up, i.e. the nearest-2x upsample the
+  // reference materialises (torch.cat([Upsample(x), y])) is never written --
+  // and [split, Cin) from the in2 view (channel stride in2_cs, offset in2_co,
+  // full resolution).  split = 0 and in_up = 0: `in` only.
+  const bf16_t* in2;
+  int in2_cs, in2_co, split, in_up;
 };
 
 // One configuration of the LDS-staged conv kernel: MR x NR 16x16 fragments

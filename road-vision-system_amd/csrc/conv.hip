@@ -219,8 +219,26 @@ static void launch_t(const ConvArgs& a, hipStream_t s) {
 // (WC) when the layer has few pixels.
 static int try_launch_patch(const ConvArgs& a, hipStream_t s, int* st);
 
+// a virtual concat / upsampled input (ConvArgs::split, in_up) is read by
+// the direct 1x1 kernel only
+static bool vcat(const ConvArgs& a) { return a.split > 0 || a.in_up; }
+
 int launch_conv(const ConvArgs& a, hipStream_t s) {
   int st = 0;
+  if (vcat(a)) {  // the direct 1x1 kernel: the widest channel tile that divides Cout and fits
+    const int T = (a.Cout + 15) / 16;
+    ConvCfg c{1, 1, 1, 1, 1, 1};
+    for (const int mr : {8, 4, 2})
+      if (T % mr == 0 && conv_cfg_ok(a, ConvCfg{mr, 1, 1, 1, 1, 1})) {
+        c.mr = mr;
+        break;
+      }
+    if (!conv_cfg_ok(a, c)) {
+      set_error("virtual concat input (split %d, up %d) needs a bf16 1x1 conv", a.split, a.in_up);
+      return RV_EINVAL;
+    }
+    return launch_conv_cfg(a, c, s);
+  }
   if (try_launch_patch(a, s, &st)) return st;
   if (a.in8) {
     set_error("fp8 conv (Cin %d, Cout %d, k%d s%d) has no patch-kernel configuration", a.Cin,
@@ -888,6 +906,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_direct_kernel(ConvArgs a) {
   }
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const bf16_t* src[NR];
+    const bf16_t* src2[NR];
     bool pv[NR];
     int pb[NR], py[NR], px[NR];
 #pragma unroll
@@ -899,16 +918,23 @@ __global__ __launch_bounds__(256, 2) void conv1x1_direct_kernel(ConvArgs a) {
       const int r = pp - pb[n] * HW;
       py[n] = r / a.Wo;
       px[n] = r - py[n] * a.Wo;
-      src[n] = a.in + (size_t)pp * a.in_cs + a.in_co + quad * 8;
+      // the `in` view's pixel: itself, or (y/2, x/2) of the half-resolution map
+      const size_t ps = a.in_up ? ((size_t)pb[n] * (a.Ho >> 1) + (py[n] >> 1)) * (a.Wo >> 1) + (px[n] >> 1)
+                                : (size_t)pp;
+      src[n] = a.in + ps * a.in_cs + a.in_co + quad * 8;
+      // the in2 view, addressed by logical channel (chunks at or above split)
+      src2[n] = a.in2 + (size_t)pp * a.in2_cs + a.in2_co + quad * 8 - a.split;
     }
     // unconditional loads (invalid pixels / channels read the zero block):
     // a branch around a load would make the compiler drain vmcnt to 0 before
     // the MFMAs, i.e. wait for the prefetched chunk as well
     auto load = [&](int c, uint4 (&B)[NR]) {
       const bool kin = c * 32 + quad * 8 < a.Cin;
+      const bool second = a.split > 0 && c * 32 >= a.split;
 #pragma unroll
       for (int n = 0; n < NR; ++n)
-        B[n] = *(const uint4*)((pv[n] && kin) ? (const void*)(src[n] + c * 32) : (const void*)g_zero16);
+        B[n] = *(const uint4*)((pv[n] && kin) ? (const void*)((second ? src2[n] : src[n]) + c * 32)
+                                              : (const void*)g_zero16);
     };
     f32x4 acc[MR][NR];
 #pragma unroll
@@ -1094,10 +1120,14 @@ static int launch_direct_t(const ConvArgs& a, int persist, hipStream_t s) {
 
 static bool direct_ok(const ConvArgs& a, const ConvCfg& c) {
   const int T = (a.Cout + 15) / 16;
+  const bool vcat_ok = (a.split == 0 && !a.in_up) ||
+                       (a.split % 32 == 0 && a.split <= a.Cin && (!a.in_up || (a.Ho % 2 == 0 && a.Wo % 2 == 0)) &&
+                        (a.split == a.Cin || (a.in2 && a.in2_cs % 8 == 0 && a.in2_co % 8 == 0)));
   return a.k == 1 && a.stride == 1 && a.pad == 0 && a.g2_cout0 <= 0 && a.Hin == a.Ho &&
          a.Win == a.Wo && (c.mr <= T || c.mr == 1) && a.in_cs % 8 == 0 && a.in_co % 8 == 0 &&
-         direct_smem(a, c.mr) <= 160 * 1024;
+         !a.in8 && vcat_ok && direct_smem(a, c.mr) <= 160 * 1024;
 }
+
 
 // stride-2 patches are ~4x the tile: only tiles whose offset registers and
 // accumulators fit without spills (NR <= 2, MR * NR <= 8) are built for S = 2
@@ -1159,7 +1189,7 @@ static const int kTiles[][2] = {{8, 2}, {8, 1}, {5, 2}, {5, 1}, {4, 4}, {4, 2}, 
 
 bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c) {
   if (c.kind == 1) return !a.in8 && direct_ok(a, c);
-  if (c.kind != 0) return false;
+  if (c.kind != 0 || vcat(a)) return false;
   if (a.in8 && !((c.mr == 1 || c.mr == 2 || c.mr == 4) && (c.nr == 1 || c.nr == 2 || c.nr == 4)))
     return false;
   if (a.in8 && (a.Cin % 16 || a.in_co % 16 || a.in_cs % 16 ||

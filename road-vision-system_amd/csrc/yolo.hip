@@ -266,7 +266,18 @@ struct Buf {
 struct TraceRec {
   int conv, in_buf, in_cs, in_co, Hin, Win, Ho, Wo;
   int out0_buf, out0_cs, out0_co, up0, out1_buf, out1_cs, out1_co, up1;
-  int res_buf, res_cs, res_co, pad;
+  int res_buf, res_cs, res_co;
+  int in_up, in2_buf, in2_cs, in2_co, split;  // virtual concat input (ConvArgs::split)
+};
+
+// A 1x1 conv's virtual concat input (ConvArgs::in2 / split / in_up):
+// channels [0, split) from view a (read upsampled 2x when up), the rest
+// from view b.
+struct VIn {
+  View a;
+  int up;
+  View b;
+  int split;
 };
 
 // Live per-launch timing of conv_mfma (bench roofline): one hipEvent pair
@@ -490,9 +501,19 @@ struct Exec {
   }
 
   // one record per conv spec (layer-wise parity tests read these back)
-  void trace(int idx, const ConvArgs& a, View in, View o0, int up0, View o1, int up1, View res) {
+  void trace(int idx, const ConvArgs& a, View in, View o0, int up0, View o1, int up1, View res,
+             const VIn* vin = nullptr) {
     TraceRec r;
     memset(&r, 0, sizeof(r));
+    r.in2_buf = -1;
+    if (vin) {
+      in = vin->a;
+      r.in_up = vin->up;
+      r.in2_buf = vin->b.buf;
+      r.in2_cs = vin->b.cs;
+      r.in2_co = vin->b.co;
+      r.split = vin->split;
+    }
     r.conv = idx;
     r.in_buf = in.buf;
     r.in_cs = in.cs;
@@ -520,6 +541,12 @@ struct Exec {
   // adds and its packed weights -- each byte once, however the kernel tiles.
   static double launch_bytes(const ConvArgs& a) {
     const double px_in = (double)a.B * a.Hin * a.Win, px_out = (double)a.B * a.Ho * a.Wo;
+    if (a.split > 0 || a.in_up) {  // virtual concat: each source read once
+      const double cin1 = a.split > 0 ? a.split : a.Cin;
+      const double src = (a.in_up ? px_in / 4 : px_in) * cin1 + px_in * (a.Cin - cin1);
+      const double outs = (a.out0 ? (a.out0_up ? 4 : 1) : 0) + (a.out1 ? (a.out1_up ? 4 : 1) : 0);
+      return 2.0 * src + 2.0 * px_out * a.Cout * outs + 2.0 * a.Cout * a.Cin;
+    }
     const bool g2 = a.g2_cout0 > 0;
     const int cout1 = g2 ? a.g2_cout0 : a.Cout, cout2 = g2 ? a.Cout - a.g2_cout0 : 0;
     double in_ch = a.Cin;
@@ -576,14 +603,22 @@ struct Exec {
   double fused_bytes = 0.0;  // algorithmic bytes of the next fused launch
 
   // conv `name`: input view at map level li -> up to two output views
+  // (vin: a 1x1 conv's virtual concat input instead of `in`)
   void conv(const std::string& name, View in, int li, View o0, int up0 = 0, View o1 = {-1, 0, 0},
-            int up1 = 0, View res = {-1, 0, 0}) {
+            int up1 = 0, View res = {-1, 0, 0}, const VIn* vin = nullptr) {
     if (status) return;
     const int idx = spec(name);
     if (idx < 0) return;
     const ConvSpec& c = M->def.convs[idx];
-    const ConvArgs a = args(c, in, li, o0, up0, o1, up1, res);
-    trace(idx, a, in, o0, up0, o1, up1, res);
+    ConvArgs a = args(c, vin ? vin->a : in, li, o0, up0, o1, up1, res);
+    if (vin) {
+      a.in_up = vin->up;
+      a.in2 = (const bf16_t*)ptr(vin->b.buf);
+      a.in2_cs = vin->b.cs;
+      a.in2_co = vin->b.co;
+      a.split = vin->split;
+    }
+    trace(idx, a, in, o0, up0, o1, up1, res, vin);
     launch(a, idx, flops_of(c, a));
   }
 
@@ -627,10 +662,11 @@ struct Exec {
   // bottlenecks + cv2 (c2f.hip; intermediates stay in LDS).
   void c2f(const std::string& p, View in, int li, int cb, int c2, int n, bool shortcut, View o0,
            int up0 = 0, View o1 = {-1, 0, 0}, int up1 = 0, bool fuse = false,
-           bool cv1_done = false) {
+           bool cv1_done = false, const VIn* vin = nullptr) {
     const int c = c2 / 2;
     const int cs = (2 + n) * c;
-    if (!cv1_done) conv(p + ".cv1", in, li, View{cb, cs, 0});
+    if (!cv1_done)
+      conv(p + ".cv1", in, li, View{cb, cs, 0}, 0, View{-1, 0, 0}, 0, View{-1, 0, 0}, vin);
     if (fuse && !status && up0 == 0 && o1.buf < 0 && c2f_fusable(c, n, cs, 0, o0.cs, o0.co)) {
       Model::FusedC2f f;
       memset(&f.a, 0, sizeof(f.a));
@@ -1054,13 +1090,25 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
   st = f8 ? launch_sppf_pool_fp8((uint8_t*)E.ptr(M->SP), B, M->map_h[5], M->map_w[5], sc, E.s)
           : launch_sppf_pool((bf16_t*)E.ptr(M->SP), B, M->map_h[5], M->map_w[5], sc, E.s);
   if (st) return st;
+  // The neck's two Upsample + Concat pairs (yolov8.yaml layers 10-11 and
+  // 13-14): bf16 plans read the upsampled half of model.12.cv1's and
+  // model.15.cv1's input straight from the half-resolution map (a virtual
+  // concat, ConvArgs::split / in_up), so the 4x upsampled copies are never
+  // written; fp8 plans (patch kernel only) and RV_VCAT=0 materialise them
+  // into CAT11[0, c5) / CAT14[0, h12) as before.
+  static const bool vcat_env = !getenv("RV_VCAT") || atoi(getenv("RV_VCAT")) != 0;
+  const bool vcat = vcat_env && !f8;
+  const View none{-1, 0, 0};
+  const VIn vin12{View{M->CAT20, cat20, v.h18}, 1, View{M->CAT11, cat11, v.c5}, v.c5};
+  const VIn vin15{View{M->CAT17, cat17, v.h15}, 1, View{M->CAT14, cat14, v.h12}, v.h12};
   E.conv("model.9.cv2", View{M->SP, 4 * sc, 0}, 5, View{M->CAT20, cat20, v.h18}, 0,
-         View{M->CAT11, cat11, 0}, 1);
+         vcat ? none : View{M->CAT11, cat11, 0}, vcat ? 0 : 1);
   // head
   E.c2f("model.12", View{M->CAT11, cat11, 0}, 4, M->C12, v.h12, v.nb, false,
-        View{M->CAT17, cat17, v.h15}, 0, View{M->CAT14, cat14, 0}, 1);
+        View{M->CAT17, cat17, v.h15}, 0, vcat ? none : View{M->CAT14, cat14, 0}, vcat ? 0 : 1,
+        false, false, vcat ? &vin12 : nullptr);
   E.c2f("model.15", View{M->CAT14, cat14, 0}, 3, M->C15, v.h15, v.nb, false,
-        View{M->X15, v.h15, 0}, 0, View{-1, 0, 0}, 0, fuse_c2f);
+        View{M->X15, v.h15, 0}, 0, View{-1, 0, 0}, 0, fuse_c2f, false, vcat ? &vin15 : nullptr);
   if (E.status) return E.status;
   M->n_part1 = (int)M->launches.size();
   M->part1_B = B;
@@ -1182,7 +1230,7 @@ extern "C" int rv_yolo_trace(void* h, int* recs, int max_recs) {
   Model* M = (Model*)h;
   const int n = (int)M->trace.size();
   if (recs)
-    for (int i = 0; i < n && i < max_recs; ++i) memcpy(recs + 20 * i, &M->trace[i], 20 * sizeof(int));
+    for (int i = 0; i < n && i < max_recs; ++i) memcpy(recs + 24 * i, &M->trace[i], 24 * sizeof(int));
   return n;
 }
 

@@ -100,12 +100,13 @@ class RoadVisionEngine:
         proc.copy_(p)
 
     def yolo_stage(self, lb: Optional[torch.Tensor], slot: int = 0, lane: int = 0,
-                   part: int = 0) -> None:
+                   part: int = 0, batch: Optional[int] = None) -> None:
         """YOLOv8 forward + decode in forward context `lane`; NMS candidates
         land in candidate slot `slot`.  part 1 / 2: the two halves of the
-        forward (YoloEngine.forward_raw)."""
+        forward (YoloEngine.forward_raw); part 2 continues part 1's batch
+        (`batch` images, default S * pair)."""
         self.detector.forward_raw(lb, slot=slot, lane=lane, part=part,
-                                  batch=self.S if lb is not None else self.S * self.pair)
+                                  batch=batch if batch is not None else self.S * self.pair)
 
     def detect_stage(self, frames: torch.Tensor, slot: int = 0) -> torch.Tensor:
         proc, lb = self.preprocess_stage(frames)

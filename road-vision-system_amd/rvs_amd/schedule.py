@@ -5,8 +5,10 @@ The reference's per-frame chain is synchronous (main_preview.py:94-109:
 ``pipeline(raw) -> detector.infer(proc) -> tracker.update(dets, ts, proj)``).
 On the device the three stages of consecutive steps are independent except
 through SORT's per-stream state, so a run of K steps is software-pipelined
-over four HIP streams.  A *unit* is P = ``eng.pair`` consecutive steps (one
-YOLO forward over their P*S frames); unit u has four stages
+over four HIP streams.  A *unit* is P consecutive steps (one YOLO forward
+over their P*S frames; P = ``eng.pair`` by default, or a per-unit size list
+``units`` whose largest entry is at most ``eng.pair`` -- small units at the
+two ends shorten the pipeline's fill and drain); unit u has four stages
 
     P(u)   preprocess of its P steps into letterbox slot u % 4   (stream sp)
     Y1(u)  first half of its forward on lane u % 2                (stream sy)
@@ -192,7 +194,8 @@ class PipelinedRun:
     record, "proc": step k's proc frames}; the records hold what K step()
     calls would have produced."""
 
-    def __init__(self, eng, frames, ts, mode: str = "native", sync: str = "flow"):
+    def __init__(self, eng, frames, ts, mode: str = "native", sync: str = "flow",
+                 units: Optional[List[int]] = None):
         if mode not in ("native", "eager"):
             raise ValueError(f"mode {mode!r}: expected 'native' or 'eager'")
         if sync not in ("stage", "flow"):
@@ -201,13 +204,20 @@ class PipelinedRun:
             raise ValueError("PipelinedRun needs RoadVisionEngine(lanes=2)")
         P = eng.pair
         K = len(frames)
-        if K % P:
-            raise ValueError(f"the step count {K} is not a multiple of pair={P}")
+        if units is None:
+            if K % P:
+                raise ValueError(f"the step count {K} is not a multiple of pair={P}")
+            units = [P] * (K // P)
+        units = [int(x) for x in units]
+        if sum(units) != K or min(units) < 1 or max(units) > P:
+            raise ValueError(f"unit sizes {units} must be in [1, pair={P}] and sum to {K}")
         if len(ts) != K:
             raise ValueError("frames and ts differ in length")
         self.eng, self.frames, self.ts = eng, list(frames), list(ts)
         self.mode, self.sync = mode, sync
-        self.K, self.P, self.U = K, P, K // P
+        self.K, self.P, self.U = K, P, len(units)
+        self.units = units
+        self.k0 = [sum(units[:u]) for u in range(len(units))]  # first step of unit u
         dev = eng.device
         self.records = [Record(eng.S, eng.detector.max_det, dev) for _ in range(K)]
         # proc outputs: one buffer per step, allocated here (not in the run)
@@ -228,28 +238,28 @@ class PipelinedRun:
 
     # -- the four stages of unit u ------------------------------------------
     def _prep(self, u: int) -> None:
-        eng, S, P = self.eng, self.eng.S, self.P
+        eng, S = self.eng, self.eng.S
         slot = u % eng.detector.slots
-        for h in range(P):
-            k = u * P + h
+        for h in range(self.units[u]):
+            k = self.k0[u] + h
             eng.preprocess_into(self.frames[k], self.procs[k], slot, h * S)
 
     def _y1(self, u: int) -> None:
         eng = self.eng
-        S, P, slots = eng.S, self.P, eng.detector.slots
-        eng.yolo_stage(eng.detector.lb[u % slots][:P * S], u % slots, u % 2, part=1)
+        S, slots = eng.S, eng.detector.slots
+        eng.yolo_stage(eng.detector.lb[u % slots][:self.units[u] * S], u % slots, u % 2, part=1)
 
     def _y2(self, u: int) -> None:
         slots = self.eng.detector.slots
-        self.eng.yolo_stage(None, u % slots, u % 2, part=2)
+        self.eng.yolo_stage(None, u % slots, u % 2, part=2, batch=self.units[u] * self.eng.S)
 
     def _track(self, u: int, E: "_Events") -> None:
         """NMS of the unit's P*S images, then SORT + hand-back of each step
         in order; a timing event marks each step's completion."""
-        eng, S, P = self.eng, self.eng.S, self.P
+        eng, S, P = self.eng, self.eng.S, self.units[u]
         dets, det_n = eng.detector.nms(S * P, u % eng.detector.slots)
         for h in range(P):
-            k = u * P + h
+            k = self.k0[u] + h
             eng.track_handback(dets[h * S:(h + 1) * S], det_n[h * S:(h + 1) * S], self.ts[k],
                                self.records[k])
             E.record(("done", k), self.st, timing=True)

@@ -111,15 +111,17 @@ def test_results_record_matches_device_outputs(cuda):
     eng.close()
 
 
-@pytest.mark.parametrize("mode,sync,pair", [
-    ("native", "flow", 1), ("native", "stage", 1), ("native", "flow", 2), ("native", "stage", 2),
-    ("eager", "flow", 2), ("eager", "stage", 1)])
-def test_pipelined_run_matches_sequential_steps(cuda, mode, sync, pair):
+@pytest.mark.parametrize("mode,sync,pair,units", [
+    ("native", "flow", 1, None), ("native", "stage", 1, None), ("native", "flow", 2, None),
+    ("native", "stage", 2, None), ("eager", "flow", 2, None), ("eager", "stage", 1, None),
+    ("native", "flow", 4, [1, 2, 4, 1]), ("eager", "flow", 2, [1, 1, 2, 2, 1, 1])])
+def test_pipelined_run_matches_sequential_steps(cuda, mode, sync, pair, units):
     """bench.py's timed mode (rvs_amd.schedule.PipelinedRun): units of `pair`
     steps software-pipelined over four HIP streams -- preprocess of unit u+1,
     the two forward halves of units u and u-1 on two lanes, NMS + SORT +
     hand-back of unit u-2 -- issued by the native launch list or eagerly,
-    lock-stepped or chained by per-dependency events.  EVERY step's
+    lock-stepped or chained by per-dependency events; `units`: unequal unit
+    sizes (bench.py --units ramp: short units at both ends).  EVERY step's
     handed-back detections / track ids and proc frames, and the final SORT
     state, must equal those of plain sequential step() calls; a second run()
     of the same schedule continues the tracks like K more step() calls."""
@@ -145,7 +147,7 @@ def test_pipelined_run_matches_sequential_steps(cuda, mode, sync, pair):
     for r in range(2):  # two runs over two windows of K steps
         f0 = 1 + r * K
         run = PipelinedRun(pip, [frames[f0 + k] for k in range(K)],
-                           [ts[f0 + k] for k in range(K)], mode=mode, sync=sync)
+                           [ts[f0 + k] for k in range(K)], mode=mode, sync=sync, units=units)
         if mode == "native":
             assert run.sched.num_nodes() > 0
         run.run()

@@ -63,9 +63,9 @@ class Introspect8:
         self.B = B
         self.ws = eng.ws.cpu().numpy()
         n = lib.rv_yolo_trace(eng._h, None, 0)
-        recs = np.zeros(n * 20, np.int32)
+        recs = np.zeros(n * 24, np.int32)
         lib.rv_yolo_trace(eng._h, recs.ctypes.data, n)
-        self.recs = recs.reshape(n, 20)
+        self.recs = recs.reshape(n, 24)
         self.bufs = eng.buffers(B)
         self.scales = eng.act_scales
 
@@ -158,7 +158,7 @@ def test_fp8_every_conv_layerwise(cuda, H, W, B, variant):
     worst = []
     for r in ins.recs:
         (ci_, inb, incs, inco, Hin, Win, Ho, Wo, o0, o0cs, o0co, up0, o1, o1cs, o1co, up1,
-         rb, rcs, rco, _) = r.tolist()
+         rb, rcs, rco, in_up, in2b, in2cs, in2co, split) = r.tolist()
         name, cin, cout, k, s, act = specs[ci_]
         w, b = params[name]
         if Y._fp8_conv(name):

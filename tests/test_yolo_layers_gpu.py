@@ -49,9 +49,9 @@ class Introspect:
         torch.cuda.synchronize()
         self.ws = eng.ws.cpu().numpy()
         n = self.lib.rv_yolo_trace(eng._h, None, 0)
-        recs = np.zeros(n * 20, np.int32)
+        recs = np.zeros(n * 24, np.int32)
         self.lib.rv_yolo_trace(eng._h, recs.ctypes.data, n)
-        self.recs = recs.reshape(n, 20)
+        self.recs = recs.reshape(n, 24)
         self.bufs = []
         for i in range(self.lib.rv_yolo_num_buffers(eng._h)):
             info = (ctypes.c_int * 4)()
@@ -99,10 +99,16 @@ def test_every_conv_layerwise(cuda, H, W, B, variant):
     worst = []
     for r in ins.recs:
         (ci_, inb, incs, inco, Hin, Win, Ho, Wo, o0, o0cs, o0co, up0, o1, o1cs, o1co, up1,
-         rb, rcs, rco, _) = r.tolist()
+         rb, rcs, rco, in_up, in2b, in2cs, in2co, split) = r.tolist()
         name, cin, cout, k, s, act = specs[ci_]
         w, b = params[name]
-        x = ins.view(inb)[..., inco:inco + cin]
+        if in2b >= 0:  # virtual concat: [upsampled] view 1 channels, then view 2's
+            x1 = ins.view(inb)[..., inco:inco + split]
+            if in_up:
+                x1 = x1.repeat(2, axis=1).repeat(2, axis=2)
+            x = np.concatenate([x1, ins.view(in2b)[..., in2co:in2co + cin - split]], -1)
+        else:
+            x = ins.view(inb)[..., inco:inco + cin]
         xt = torch.from_numpy(np.ascontiguousarray(x.transpose(0, 3, 1, 2))).double()
         wt = torch.from_numpy(round_bf16(w)).double()
         y = F.conv2d(xt, wt, torch.from_numpy(b).double(), stride=s, padding=k // 2)
