@@ -163,10 +163,11 @@ int rv_yolo_destroy(void* handle);
  * run the production kernel sequence, so raw_out is what the candidate
  * path computed. */
 #define RV_YOLO_OPT_RAW_UNFUSED 1
-/* RV_YOLO_OPT_FUSE_C2F (default 1): the narrow C2f blocks (hidden width 16
- * or 32: YOLOv8n model.2 / model.4 / model.15) run as cv1 + one fused
- * launch for the bottlenecks and cv2 (bit-identical to the unfused convs);
- * 0: one launch per conv. */
+/* RV_YOLO_OPT_FUSE_C2F: the narrow C2f blocks run as cv1 + one fused launch
+ * for the bottlenecks and cv2 (bit-identical to the unfused convs): 1
+ * (default) the hidden-width-16 blocks (YOLOv8n model.2), 2 also the
+ * width-32 ones (model.4 / model.15; measured slower than unfused), 0 none:
+ * one launch per conv. */
 #define RV_YOLO_OPT_FUSE_C2F 2
 /* RV_YOLO_OPT_STEM_X1 (default 0): the fused stem (conv0 + model.1, and
  * model.2.cv1 from its registers) also writes the X1 map; by default X1

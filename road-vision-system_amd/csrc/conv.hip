@@ -26,6 +26,7 @@ typedef __attribute__((ext_vector_type(8))) int i32x8;
 
 typedef __attribute__((ext_vector_type(2))) float f32x2v;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
+typedef __attribute__((ext_vector_type(2))) unsigned int v2u32;
 
 // f32 -> bf16, round to nearest even, on the hardware converter
 // (v_cvt_pk_bf16_f32: two values per instruction).
@@ -321,7 +322,60 @@ struct PatchGeo {
   int pinst;       // DMA instructions for the patch (64 x 16-B slots each)
   int tiles_x, tiles_y;
   int p_bytes;     // pinst * 1024
+  int fast;        // epilogue_fast applies (epi_fast)
 };
+
+// The common epilogue (one bf16 output view, no upsampled copy, optional
+// bf16 residual, Cout a multiple of 16, every byte offset < 2^31) runs
+// epilogue_fast: buffer stores / loads whose per-lane byte offsets are one
+// 24-bit multiply per pixel, each 16-channel fragment m in the instruction's
+// immediate offset -- no 64-bit address arithmetic per (pixel, fragment).
+static bool epi_fast(const ConvArgs& a) {
+  static const bool off = getenv("RV_EPI_SLOW") != nullptr;  // A/B: the generic epilogue
+  const double px = (double)a.B * a.Ho * a.Wo;
+  return !off && !a.out_f32 && !a.out1 && !a.out0_up && !a.in8 && a.Cout % 16 == 0 && px < (1 << 23) &&
+         a.out0_cs < 2048 && px * a.out0_cs * 2 < 2147483647.0 &&
+         (!a.res || (a.res_cs < 2048 && px * a.res_cs * 2 < 2147483647.0));
+}
+
+// lane pixel opx (output pixel index b*Ho*Wo + y*Wo + x; valid = pv) of
+// each n; cout0 the block's first output channel
+template <int MR, int NR>
+__device__ __forceinline__ void epilogue_fast(const ConvArgs& a, f32x4 (&acc)[MR][NR], int cout0,
+                                              const bool (&pv)[NR], const uint32_t (&opx)[NR],
+                                              int quad, const f32x4 (&bias)[MR]) {
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(a.out0, 0, 0x7FFFFFFF, kRsrcFlags);
+  const __amdgpu_buffer_rsrc_t rr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.res, 0, 0x7FFFFFFF, kRsrcFlags);
+  const int cq = cout0 + quad * 4;
+#pragma unroll
+  for (int n = 0; n < NR; ++n) {
+    if (!pv[n]) continue;
+    const uint32_t vo = (__umul24(opx[n], (uint32_t)a.out0_cs) + a.out0_co + cq) * 2;
+    const uint32_t vr = a.res ? (__umul24(opx[n], (uint32_t)a.res_cs) + a.res_co + cq) * 2 : 0u;
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      if (cout0 + m * 16 >= a.Cout) continue;  // block-uniform (Cout % 16 == 0)
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[m][n][i] + bias[m][i];
+      if (a.act) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = silu(v[i]);
+      }
+      if (a.res) {
+        const uint2 q = __builtin_bit_cast(
+            uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(vr + m * 32), 0, 0));
+        v[0] += bf2f(q.x & 0xFFFF);
+        v[1] += bf2f(q.x >> 16);
+        v[2] += bf2f(q.y & 0xFFFF);
+        v[3] += bf2f(q.y >> 16);
+      }
+      const uint2 pk = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, pk), ro, (int)(vo + m * 32), 0, 0);
+    }
+  }
+}
 
 // LDS quarter swizzle of 64-B pixel / weight-row slots: slot quarter q of
 // slot i holds source quarter q ^ swzq(i).  bf16 fragments are read with
@@ -832,10 +886,16 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
         px[n] = tx * g.C + ocol[n];
         pv[n] = oin[n] && py[n] < a.Ho && px[n] < a.Wo;
       }
-      if constexpr (F8)
+      if constexpr (F8) {
         epilogue8<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias, dq);
-      else
+      } else if (g.fast) {
+        uint32_t opx[NR];
+#pragma unroll
+        for (int n = 0; n < NR; ++n) opx[n] = (uint32_t)((b * a.Ho + py[n]) * a.Wo + px[n]);
+        epilogue_fast<MR, NR>(a, acc, cout0, pv, opx, quad, bias);
+      } else {
         epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias);
+      }
       ti += gridDim.x;
       grp = 0;
     } else {
@@ -860,7 +920,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
 // two are bit-identical.
 // ---------------------------------------------------------------------------
 template <int MR, int NR>
-__global__ __launch_bounds__(256, 2) void conv1x1_direct_kernel(ConvArgs a) {
+__global__ __launch_bounds__(256, 2) void conv1x1_direct_kernel(ConvArgs a, int fast) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int BC = 16 * MR;
   constexpr int W_BYTES = BC * 64;  // one 32-channel chunk of the block's weights
@@ -967,7 +1027,14 @@ __global__ __launch_bounds__(256, 2) void conv1x1_direct_kernel(ConvArgs a) {
       if (c + 1 < nch) mma(c + 1, B1);
       __builtin_amdgcn_sched_barrier(0);
     }
-    epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias);
+    if (fast) {
+      uint32_t opx[NR];
+#pragma unroll
+      for (int n = 0; n < NR; ++n) opx[n] = (uint32_t)(t * 64 * NR + wave * 16 * NR + n * 16 + col);
+      epilogue_fast<MR, NR>(a, acc, cout0, pv, opx, quad, bias);
+    } else {
+      epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias);
+    }
   }
 }
 
@@ -1008,6 +1075,7 @@ static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& 
   g.tiles_y = ceil_div(a.Ho, g.R);
   const int nch = conv_nch(a);
   g.G = std::max(1, std::min(c.G, nch));
+  g.fast = epi_fast(a) ? 1 : 0;
   // per-lane offset registers of the kernel (patch_maxit)
   const int maxit = (a.stride == 2 ? 6 : 2) * NR + 2;
   if (ceil_div(g.pinst, 4) > maxit) return false;
@@ -1114,7 +1182,7 @@ static int launch_direct_t(const ConvArgs& a, int persist, hipStream_t s) {
   const int ntiles = ceil_div(a.B * a.Ho * a.Wo, 64 * NR);
   int gx = ntiles;
   if (persist) gx = std::min(ntiles, std::max(1, num_cus() * occ / ytiles));
-  fn<<<dim3(gx, ytiles), 256, smem, s>>>(a);
+  fn<<<dim3(gx, ytiles), 256, smem, s>>>(a, epi_fast(a) ? 1 : 0);
   return launch_status("conv1x1_direct");
 }
 

@@ -336,6 +336,7 @@ struct Model {
   // unfused stem, so every activation (X0 included) is in the workspace
   int raw_unfused = 1;
   // RV_YOLO_OPT_FUSE_C2F: narrow C2f blocks as cv1 + one fused chain launch
+  // (1: the hidden-width-16 chains only, 2: width 16 and 32, 0: none)
   int fuse_c2f = 1;
   // RV_YOLO_OPT_STEM_X1: the fused stem also writes X1 (parity tests)
   int stem_x1 = 0;
@@ -920,7 +921,7 @@ extern "C" int rv_yolo_set_option(void* h, int opt, int value) {
       M->raw_unfused = value != 0;
       return RV_OK;
     case RV_YOLO_OPT_FUSE_C2F:
-      M->fuse_c2f = value != 0;
+      M->fuse_c2f = value < 0 ? 0 : (value > 2 ? 2 : value);
       return RV_OK;
     case RV_YOLO_OPT_STEM_X1:
       M->stem_x1 = value != 0;
@@ -1002,6 +1003,13 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
   // activation (RV_YOLO_OPT_RAW_UNFUSED) or RV_FUSE_C2F=0
   static const bool c2f_env = !getenv("RV_FUSE_C2F") || atoi(getenv("RV_FUSE_C2F")) != 0;
   const bool fuse_c2f = c2f_env && !f8 && M->fuse_c2f && !(raw_out && M->raw_unfused);
+  // the hidden-width-32 chains (model.4, model.15 of YOLOv8n) measured
+  // faster unfused since the patch kernel's buffer-DMA / fast-epilogue work
+  // (r03: 188 + 86 us per 128-frame unit fused, 142 + 79 unfused): only
+  // the C = 16 chain (model.2 at P2, 122 fused vs 191 unfused) stays fused
+  // unless RV_FUSE_C2F32=1 or RV_YOLO_OPT_FUSE_C2F = 2
+  static const bool c2f32_env = getenv("RV_FUSE_C2F32") && atoi(getenv("RV_FUSE_C2F32")) != 0;
+  const bool fuse_c2f32 = fuse_c2f && (c2f32_env || M->fuse_c2f == 2);
   const int cat14 = v.h12 + v.c3, cat11 = v.c5 + v.c4, cat20 = v.h18 + v.c5,
             cat17 = v.h15 + v.h12;
   int st;
@@ -1077,7 +1085,7 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
         View{-1, 0, 0}, 0, fuse_c2f, stem_cv1);
   E.conv("model.3", View{M->X2, v.c2, 0}, 2, View{M->X3, v.c3, 0});
   E.c2f("model.4", View{M->X3, v.c3, 0}, 3, M->C4, v.c3, v.nm, true,
-        View{M->CAT14, cat14, v.h12}, 0, View{-1, 0, 0}, 0, fuse_c2f);
+        View{M->CAT14, cat14, v.h12}, 0, View{-1, 0, 0}, 0, v.c3 / 2 == 16 ? fuse_c2f : fuse_c2f32);
   E.conv("model.5", View{M->CAT14, cat14, v.h12}, 3, View{M->X5, v.c4, 0});
   E.c2f("model.6", View{M->X5, v.c4, 0}, 4, M->C6, v.c4, v.nm, true,
         View{M->CAT11, cat11, v.c5});
@@ -1108,7 +1116,8 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
         View{M->CAT17, cat17, v.h15}, 0, vcat ? none : View{M->CAT14, cat14, 0}, vcat ? 0 : 1,
         false, false, vcat ? &vin12 : nullptr);
   E.c2f("model.15", View{M->CAT14, cat14, 0}, 3, M->C15, v.h15, v.nb, false,
-        View{M->X15, v.h15, 0}, 0, View{-1, 0, 0}, 0, fuse_c2f, false, vcat ? &vin15 : nullptr);
+        View{M->X15, v.h15, 0}, 0, View{-1, 0, 0}, 0, v.h15 / 2 == 16 ? fuse_c2f : fuse_c2f32,
+        false, vcat ? &vin15 : nullptr);
   if (E.status) return E.status;
   M->n_part1 = (int)M->launches.size();
   M->part1_B = B;

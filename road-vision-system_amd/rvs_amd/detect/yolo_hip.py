@@ -206,11 +206,14 @@ class YoloEngine:
         for h in self._hs:
             call("rv_yolo_set_option", h, 3, 1 if on else 0)
 
-    def set_fuse_c2f(self, on: bool) -> None:
-        """Narrow C2f blocks as one fused launch (default) or one launch per
-        conv (RV_YOLO_OPT_FUSE_C2F; bit-identical results)."""
+    def set_fuse_c2f(self, on) -> None:
+        """Narrow C2f blocks as one fused launch or one launch per conv
+        (RV_YOLO_OPT_FUSE_C2F; bit-identical results): True / 1 = the
+        hidden-width-16 chains only (default), 2 = widths 16 and 32,
+        False / 0 = none."""
+        v = 1 if on is True else (0 if on is False else int(on))
         for h in self._hs:
-            call("rv_yolo_set_option", h, 2, 1 if on else 0)
+            call("rv_yolo_set_option", h, 2, v)
 
     def letterbox(self, frames: torch.Tensor, slot: int = 0, off: int = 0) -> torch.Tensor:
         """Letterbox into images [off, off + B) of letterbox slot `slot`."""

@@ -304,7 +304,7 @@ def test_fused_c2f_is_bit_identical(cuda, H, W, B, variant):
     eng.set_raw_fused(True)
     outs = []
     for fuse in (False, True):
-        eng.set_fuse_c2f(fuse)
+        eng.set_fuse_c2f(2 if fuse else 0)  # every fusable chain (the default fuses C = 16 only)
         raw = torch.full((B, 84, eng.A), float("nan"), dtype=torch.float32, device=cuda)
         eng.forward_raw(lb, raw, slot=int(fuse))
         torch.cuda.synchronize()
