@@ -1385,6 +1385,10 @@ extern "C" int rv_yolo_autotune(void* h, const uint8_t* lb, int B, void* ws, siz
     const int n = std::min(conv_candidates(a, cands.data(), (int)cands.size()), (int)cands.size());
     for (int j = 0; j < n && !st; ++j) {
       const float t = time_cfg(&cands[j]);
+      if (dbg >= 2)
+        fprintf(stderr, "[autotune]   launch %2zu cand MR=%d NR=%d G=%d resw=%d persist=%d kind=%d %7.1f us\n",
+                i, cands[j].mr, cands[j].nr, cands[j].G, cands[j].resw, cands[j].persist,
+                cands[j].kind, t * 1e3);
       if (verify) {
         unsigned diff = 0;
         for (int d = 0; d < 2; ++d) {
