@@ -1962,7 +1962,83 @@ __device__ __forceinline__ float head_sigmoid(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
 }
 
-template <int REG, bool FUSED>
+// The fused head's MFMA section with compile-time trip counts (KB box /
+// KC class 32-channel k-steps, NCF class fragments: YOLOv8n's head is
+// KB = 2, KC = 3, NCF = 5): every A / B fragment load of the wave is issued
+// before the first MFMA, so the wave waits out one L2 latency instead of
+// one per (fragment, k-step) -- the runtime-bound loops compiled to a
+// load / s_waitcnt vmcnt(0) / MFMA chain.  Same k order and sums as the
+// generic loops (bit-identical logits).
+template <int REG, int KB, int KC, int NCF>
+__device__ __forceinline__ void head_mfma_fixed(const HeadLevel& L, float* lg, int b, int HW, int r0,
+                                                int na, int nc) {
+  constexpr int MB = REG / 4;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
+  const int an0 = wave * 16 + col;
+  const bool ok = an0 < na;
+  const bf16_t* fp = L.feat + ((size_t)b * HW + r0 + (ok ? an0 : 0)) * L.feat_cs + quad * 8;
+  constexpr int cinb = KB * 32, cinc = KC * 32;
+  uint4 Bb[KB], Bc[KC], Ab[KB][MB], Ac[KC][NCF];
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    Bb[k] = ok && k * 32 + quad * 8 < L.cin_b ? *(const uint4*)(fp + k * 32) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+      Ab[k][m] = *(const uint4*)(L.w_box + (size_t)(m * 16 + col) * cinb + k * 32 + quad * 8);
+  }
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    Bc[k] = ok && k * 32 + quad * 8 < L.cin_c ? *(const uint4*)(fp + 4 * REG + k * 32)
+                                              : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < NCF; ++m)
+      Ac[k][m] = *(const uint4*)(L.w_cls + (size_t)(m * 16 + col) * cinc + k * 32 + quad * 8);
+  }
+  float* row = lg + (size_t)(wave * 16 + col) * (L.cs + 4);
+  {
+    f32x4 acc[MB];
+#pragma unroll
+    for (int m = 0; m < MB; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KB; ++k)
+#pragma unroll
+      for (int m = 0; m < MB; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, Ab[k][m]),
+                                                         __builtin_bit_cast(bf16x8, Bb[k]), acc[m], 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      const int co = m * 16 + quad * 4;
+      *(f32x4*)(row + co) = acc[m] + *(const f32x4*)(L.b_box + co);
+    }
+  }
+  {
+    f32x4 acc[NCF];
+#pragma unroll
+    for (int m = 0; m < NCF; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int m = 0; m < NCF; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, Ac[k][m]),
+                                                         __builtin_bit_cast(bf16x8, Bc[k]), acc[m], 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < NCF; ++m) {
+      const int co = m * 16 + quad * 4;
+      const f32x4 v = acc[m] + *(const f32x4*)(L.b_cls + co);
+      float* d = row + 4 * REG + co;
+      if (co + 3 < nc) {
+        *(f32x4*)d = v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (co + i < nc) d[i] = v[i];
+      }
+    }
+  }
+}
+
+template <int REG, bool FUSED, int KB = 0, int KC = 0, int NCF = 0>
 __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B, int nc,
                                                             float conf, float* __restrict__ raw,
                                                             Cand* __restrict__ cand, int cap,
@@ -1990,7 +2066,17 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
   const int na = min(64, HW - r0);
   const int tid = threadIdx.x;
   const int cs4 = L.cs / 4, ls4 = cs4 + 1;  // row length / LDS row stride in float4
-  if constexpr (FUSED) {
+  if constexpr (FUSED && KC > 0) {
+    head_mfma_fixed<REG, KB, KC, NCF>(L, lg, b, HW, r0, na, nc);
+    __syncthreads();
+    if (L.logits_out) {  // parity/debug copy of the logits (coalesced rows)
+      f32x4* dst = (f32x4*)(L.logits_out + ((size_t)b * HW + r0) * L.cs);
+      for (int i = tid; i < na * cs4; i += 256) {
+        const int row = i / cs4, c4 = i - (i / cs4) * cs4;
+        dst[i] = ((const f32x4*)lg)[row * ls4 + c4];
+      }
+    }
+  } else if constexpr (FUSED) {
     constexpr int MB = REG / 4;  // box fragments (4*REG couts)
     const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
     const int an0 = wave * 16 + col;  // this lane's anchor (B column / D column)
@@ -2216,14 +2302,19 @@ int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_ma
   }
   const size_t smem = (size_t)64 * (cs + 4) * 4;
   const bool fused = lv[0].feat != nullptr;
-  static bool attr[2] = {false, false};
-  if (!attr[fused] && smem > 64 * 1024) {  // only raise the cap when the head needs it
+  // YOLOv8n's fused head (every level: box 64 -> 64, class 80 -> 80): the
+  // compile-time MFMA section
+  bool fixed = fused && nc == 80;
+  for (int i = 0; i < nlv && fixed; ++i)
+    fixed = lv[i].cin_b == 64 && lv[i].cin_c == 80;
+  static const bool fixed_env = !getenv("RV_DECODE_FIXED") || atoi(getenv("RV_DECODE_FIXED")) != 0;
+  fixed = fixed && fixed_env;
+  if (smem > 64 * 1024) {  // only raise the cap when the head needs it (large nc)
     // best effort: a failure surfaces as the launch error reported below
     (void)hipFuncSetAttribute(fused ? (const void*)detect_decode_kernel<16, true>
                               : (const void*)detect_decode_kernel<16, false>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();
-    attr[fused] = true;
   }
   if (cand && cand_cap < h.blk[nlv] * 64) {
     set_error("detect decode: cand_cap %d < %d segments x 64", cand_cap, h.blk[nlv]);
@@ -2235,8 +2326,12 @@ int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_ma
         set_error("fused head: bad level %d geometry", i);
         return RV_EINVAL;
       }
-    detect_decode_kernel<16, true><<<dim3(h.blk[nlv], B), 256, smem, s>>>(h, B, nc, conf, raw, cand,
-                                                                          cand_cap, cand_n);
+    if (fixed)
+      detect_decode_kernel<16, true, 2, 3, 5><<<dim3(h.blk[nlv], B), 256, smem, s>>>(
+          h, B, nc, conf, raw, cand, cand_cap, cand_n);
+    else
+      detect_decode_kernel<16, true><<<dim3(h.blk[nlv], B), 256, smem, s>>>(h, B, nc, conf, raw, cand,
+                                                                            cand_cap, cand_n);
   } else {
     detect_decode_kernel<16, false><<<dim3(h.blk[nlv], B), 256, smem, s>>>(h, B, nc, conf, raw,
                                                                            cand, cand_cap, cand_n);

@@ -521,7 +521,20 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
 struct LbFuse {
   LbGeo g;
   uint8_t* out;  // B x out_h x out_w x 3
+  // every tap of both axes has weight (2048, 0): an exact integer
+  // decimation (1080p -> 640 wide: source pixel 3d + 1), where
+  // cv2.resize(INTER_LINEAR) returns the source byte itself
+  // (lb_vmix(2048 p, ., 2048, 0) = p), so the blend is a copy
+  int copy;
 };
+
+static bool lb_is_copy(const LbGeo& G, int H, int W) {
+  for (int dx = 0; dx < G.new_w; ++dx)
+    if (lb_tap_x(dx, G.scale_x, W).w1 != 0) return false;
+  for (int dy = 0; dy < G.new_h; ++dy)
+    if (lb_tap_y(dy, G.scale_y, H).w1 != 0) return false;
+  return true;
+}
 
 __device__ __forceinline__ int clahe_cell_index(int p, float inv) {
   return (int)floorf((float)p * inv - 0.5f);
@@ -840,6 +853,12 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
         const uint8_t* r0 = tile + (ty.s0 - y0) * kM3Stride;
         const uint8_t* r1 = tile + (ty.s1 - y0) * kM3Stride;
         uint8_t* dst = lbo + jy * orow + jx * 3;
+        if (lb.copy) {
+          dst[0] = r0[c0];
+          dst[1] = r0[c0 + 1];
+          dst[2] = r0[c0 + 2];
+          continue;
+        }
         // lb_vmix with 24-bit multiplies (u8 x 11-bit weights, (d >> 4) <
         // 2^15): the full-rate v_mul_u32_u24 instead of v_mul_lo_u32
 #pragma unroll
@@ -1109,6 +1128,7 @@ extern "C" int rv_clahe_median_letterbox_u8(const uint8_t* in, uint8_t* out, int
   LbFuse lb;
   lbgeo_from(geo, H, W, lb.g);
   lb.out = lb_out;
+  lb.copy = lb_is_copy(lb.g, H, W) ? 1 : 0;
   hipStream_t s = as_stream(stream);
   uint8_t* lut = (uint8_t*)ws;
   st = launch_letterbox_pad(lb_out, B, lb.g, s);
