@@ -251,6 +251,16 @@ class BenchJob:
         soon as that step's record has been handed back (materialise=False:
         only the host time each step became available)."""
         names, n_det, busy, done = self.eng.names, 0, 0.0, []
+        # A/B probes: RV_CONSUMER_DEFER=1 builds every list after the last
+        # step's hand-back (still inside the timed region); RV_CONSUMER_NOGC=1
+        # keeps the garbage collector off while the lists are built
+        defer = os.environ.get("RV_CONSUMER_DEFER", "0") != "0"
+        nogc = os.environ.get("RV_CONSUMER_NOGC", "0") != "0"
+        if nogc:
+            import gc
+            gc.disable()
+        if defer:
+            wait_step(len(self.records) - 1)
         for k, rec in enumerate(self.records):
             wait_step(k)
             t = time.perf_counter()
@@ -258,6 +268,8 @@ class BenchJob:
             if materialise:
                 n_det += sum(len(x) for x in rec.detections(names))
                 busy += time.perf_counter() - t
+        if nogc:
+            gc.enable()
         self.cons = {"detections": n_det, "busy_s": busy, "end": time.perf_counter(),
                      "done": done}
 

@@ -224,6 +224,14 @@ class PipelinedRun:
         self.procs = [torch.empty((eng.S, eng.H, eng.W, 3), dtype=torch.uint8, device=dev)
                       for _ in range(K)]
         self.sm, self.sp, self.sy, self.st = (torch.cuda.Stream(dev) for _ in range(4))
+        import os
+        if os.environ.get("RV_PREP_PRIORITY"):  # A/B probe: the preprocess stream's priority
+            self.sp = torch.cuda.Stream(dev, priority=int(os.environ["RV_PREP_PRIORITY"]))
+        # RV_TRACK_ON_Y2=1: the track stage T(u) runs on the second-half
+        # stream right behind Y2(u) (its only producer), one stream fewer
+        # competing for the process's hardware queues
+        if os.environ.get("RV_TRACK_ON_Y2", "0") != "0":
+            self.st = self.sm
         self.sched = None
         self._events = None
         if mode == "native":
