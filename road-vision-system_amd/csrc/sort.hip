@@ -362,19 +362,10 @@ __device__ __forceinline__ void sort_update_row(Track* __restrict__ pool, const 
   }
 }
 
-// FUSED (default, rv_sort_update): the whole frame of one stream in this
-// one workgroup -- the KF predict of every live track straight into the
-// LDS boxes (sort_predict_kernel's work), the association and bookkeeping,
-// then every detection row's update (sort_update_kernel's work) after a
-// block barrier; the same arithmetic per track / detection, so the same
-// results as the three launches (RV_SORT_FUSED=0), without their two
-// launch gaps and the workspace round trip.
-template <bool FUSED>
 __global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
     StreamHdr* __restrict__ hdr, int* __restrict__ order, Track* __restrict__ pool,
     const float* __restrict__ dets, const int* __restrict__ dcount,
-    const double* __restrict__ ts_arr, SortParams p, SortWs ws, int* __restrict__ out_id,
-    double* __restrict__ out_dist, double* __restrict__ out_speed) {
+    const double* __restrict__ ts_arr, SortParams p, SortWs ws) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   float4* tbox = (float4*)smem;                     // tmax
   float4* dbox = tbox + p.tmax;                     // dmax
@@ -403,18 +394,9 @@ __global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
   Track* pl = pool + (size_t)s * p.tmax;
 
   for (int t = tid; t < T; t += kAssocThreads) {
-    const int slot = ord_g[t];
-    if constexpr (FUSED) {  // sort_predict_kernel's work, into LDS
-      Track& tr = pl[slot];
-      kf_predict(tr, ts - tr.t_pred);
-      tr.t_pred = ts;
-      tbox[t] = x_to_bbox(tr.x);
-      tupd[t] = tr.t_upd;
-    } else {
-      tbox[t] = ws.tbox[(size_t)s * p.tmax + t];
-      tupd[t] = ws.tupd[(size_t)s * p.tmax + t];
-    }
-    ord[t] = slot;
+    tbox[t] = ws.tbox[(size_t)s * p.tmax + t];
+    tupd[t] = ws.tupd[(size_t)s * p.tmax + t];
+    ord[t] = ord_g[t];
     trk_match[t] = -1;
   }
   for (int d = tid; d < D; d += kAssocThreads) {
@@ -586,7 +568,7 @@ __global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
         j = make_int2(r < n_fit ? newslot[r] : -1, h.next_id + r);
       }
     }
-    job[d] = j;  // FUSED: read back by this same thread after the barrier below
+    job[d] = j;
   }
   if (tid == 0) {
     StreamHdr o;
@@ -595,14 +577,6 @@ __global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
     o.overflow = h.overflow | (new_alive && n_new > room ? 1 : 0);
     o.pad = 0;
     hdr[s] = o;
-  }
-  if constexpr (FUSED) {
-    // the streak resets above and the predicted states are global writes of
-    // other threads: make them visible to the block before the updates
-    __threadfence_block();
-    __syncthreads();
-    for (int d = tid; d < p.dmax; d += kAssocThreads)
-      sort_update_row(pool, dets, ts, s, d, job[d], p, out_id, out_dist, out_speed);
   }
 }
 
@@ -760,14 +734,12 @@ extern "C" int rv_sort_update(void* state_in, void* state_out, int S, int tmax,
   if (r) return r;
   static int attr_set = 0;
   if ((int)smem > attr_set) {  // once per growth, outside steady-state launches
-    for (const void* fn : {(const void*)sort_associate_kernel<true>,
-                           (const void*)sort_associate_kernel<false>}) {
-      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-      if (e != hipSuccess) {
-        set_error("hipFuncSetAttribute(%zu B LDS): %s", smem, hipGetErrorString(e));
-        (void)hipGetLastError();
-        return -(int)e;
-      }
+    hipError_t e = hipFuncSetAttribute((const void*)sort_associate_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) {
+      set_error("hipFuncSetAttribute(%zu B LDS): %s", smem, hipGetErrorString(e));
+      (void)hipGetLastError();
+      return -(int)e;
     }
     attr_set = (int)smem;
   }
@@ -779,20 +751,12 @@ extern "C" int rv_sort_update(void* state_in, void* state_out, int S, int tmax,
   w.tbox = (float4*)((uint8_t*)ws + off[1]);
   w.tupd = (double*)((uint8_t*)ws + off[2]);
   w.det_job = (int2*)((uint8_t*)ws + off[3]);
-  // one launch per frame (sort_associate_kernel<true>: predict + associate +
-  // update); RV_SORT_FUSED=0: the three-launch form
-  static const bool fused = !getenv("RV_SORT_FUSED") || atoi(getenv("RV_SORT_FUSED")) != 0;
-  if (fused) {
-    sort_associate_kernel<true><<<S, kAssocThreads, smem, st>>>(v.hdr, v.order, v.pool, dets, dcount,
-                                                               ts, p, w, out_id, out_dist, out_speed);
-    return launch_status("rv_sort_update (fused)");
-  }
   sort_predict_kernel<<<dim3(ceil_div(tmax, 256), S), 256, 0, st>>>(v.hdr, v.order, v.pool, ts,
                                                                      tmax, w);
   r = launch_status("rv_sort_update (predict)");
   if (r) return r;
-  sort_associate_kernel<false><<<S, kAssocThreads, smem, st>>>(v.hdr, v.order, v.pool, dets, dcount,
-                                                              ts, p, w, nullptr, nullptr, nullptr);
+  sort_associate_kernel<<<S, kAssocThreads, smem, st>>>(v.hdr, v.order, v.pool, dets, dcount, ts, p,
+                                                       w);
   r = launch_status("rv_sort_update (associate)");
   if (r) return r;
   sort_update_kernel<<<dim3(ceil_div(dmax, 256), S), 256, 0, st>>>(v.pool, dets, ts, p, w, out_id,
