@@ -1,7 +1,8 @@
 """Per-dispatch counters of the last bench step from rocprofv3
 counter_collection.csv files (one per --pmc pass), merged by dispatch order.
 Usage: pmc_report.py csv [csv ...]  -> table on stdout.  The last step starts
-at the last clahe_lut_kernel dispatch."""
+at the last letterbox_pad_kernel dispatch before the last clahe_lut_kernel
+(or at that clahe_lut_kernel)."""
 import csv
 import sys
 from collections import OrderedDict
@@ -13,7 +14,11 @@ def load(path):
         d = disp.setdefault(int(r["Dispatch_Id"]), {"name": r["Kernel_Name"]})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     rows = list(disp.values())
-    start = max(i for i, d in enumerate(rows) if "clahe_lut_kernel" in d["name"])
+    last = max(i for i, d in enumerate(rows) if "clahe_lut_kernel" in d["name"])
+    # the fused preprocess runs one LUT launch per frame group (RV_PRE_GROUP),
+    # all after the step's letterbox_pad_kernel
+    pads = [i for i, d in enumerate(rows[:last]) if "letterbox_pad_kernel" in d["name"]]
+    start = pads[-1] if pads else last
     return rows[start:]
 
 
