@@ -78,16 +78,30 @@ __device__ __forceinline__ int clahe_luma(int b, int g, int r) {
 // single-read pass below): wave 0 stores it as 64 `sc1` dwords (each 128-B
 // line whole in one store instruction), the hand-off form of
 // MI355X_MICROARCH.md "Valid forms" (sc1 stores, agent counter, sc1 loads).
+// Slice mode (the single-read pass): the workgroup histograms tile rows
+// [r_lo, r_hi) only, stores that partial histogram (sc1) in `part` slot
+// `slice` of `nslice`, and the workgroup whose agent-scope add to the tile's
+// counter comes last sums the partials (sc1 loads) and builds the LUT.
+// Returns whether this workgroup built (and published) the LUT.
+struct LutSlice {
+  int r_lo, r_hi, slice, nslice;
+  int* part;      // nslice x 256 partial histograms of this tile
+  int* tile_ctr;  // slices finished for this tile
+};
+
 template <int SPACE, bool SC1>
-__device__ __forceinline__ void clahe_lut_body(const uint8_t* __restrict__ in,
+__device__ __forceinline__ bool clahe_lut_body(const uint8_t* __restrict__ in,
                                                uint8_t* __restrict__ lut, int H, int W, int pitch,
-                                               const ClaheGeo& g, int tile, int b, int t) {
+                                               const ClaheGeo& g, int tile, int b, int t,
+                                               const LutSlice* sl = nullptr) {
   constexpr int kCopies = 16;
   constexpr int kWords = 256 * kCopies;
   __shared__ int hist[kWords];
   __shared__ int wsum[4], wtot[4];
   __shared__ uint32_t lut_w[64];
+  __shared__ int s_last;
   const int wave = t >> 6;
+  const int r_lo = sl ? sl->r_lo : 0, r_hi = sl ? sl->r_hi : g.th;
   const int ty = tile / g.tiles, tx = tile - (tile / g.tiles) * g.tiles;
   const int x0 = tx * g.tw, y0 = ty * g.th;
   const uint8_t* frame = in + (size_t)b * H * pitch;
@@ -102,7 +116,7 @@ __device__ __forceinline__ void clahe_lut_body(const uint8_t* __restrict__ in,
   auto bump = [&](int y) { atomicAdd(&h[y * kCopies], 1); };
   if (vec) {
     const int groups = g.tw >> 2;
-    const int total = groups * g.th;
+    const int total = groups * (r_hi - r_lo);
     // 4 groups in flight per thread (the loop is load-latency bound)
     for (int i0 = t; i0 < total; i0 += 4 * 256) {
       uint32_t w[4][3];
@@ -114,7 +128,7 @@ __device__ __forceinline__ void clahe_lut_body(const uint8_t* __restrict__ in,
           const int r = i / groups;
           const int gi = i - r * groups;
           const uint32_t* p =
-              (const uint32_t*)(frame + (size_t)(y0 + r) * pitch + (size_t)(x0 + gi * 4) * 3);
+              (const uint32_t*)(frame + (size_t)(y0 + r_lo + r) * pitch + (size_t)(x0 + gi * 4) * 3);
           w[u][0] = p[0];
           w[u][1] = p[1];
           w[u][2] = p[2];
@@ -132,9 +146,9 @@ __device__ __forceinline__ void clahe_lut_body(const uint8_t* __restrict__ in,
       }
     }
   } else {
-    const int total = g.tw * g.th;
+    const int total = g.tw * (r_hi - r_lo);
     for (int i = t; i < total; i += 256) {
-      const int r = i / g.tw;
+      const int r = r_lo + i / g.tw;
       const int c = i - r * g.tw;
       int sy = y0 + r;
       if (sy >= H) sy = reflect101(sy, H);
@@ -149,6 +163,20 @@ __device__ __forceinline__ void clahe_lut_body(const uint8_t* __restrict__ in,
   int v = 0;
 #pragma unroll
   for (int c = 0; c < kCopies; ++c) v += hist[t * kCopies + ((c + t) & (kCopies - 1))];
+  if (sl) {
+    // each wave stores 64 consecutive ints: two whole 128-B lines per store
+    __hip_atomic_store(sl->part + sl->slice * 256 + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0)
+      s_last = __hip_atomic_fetch_add(sl->tile_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               sl->nslice - 1;
+    __syncthreads();
+    if (!s_last) return false;
+    v = 0;
+    for (int k = 0; k < sl->nslice; ++k)
+      v += __hip_atomic_load(sl->part + k * 256 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (g.clip_limit > 0) {
     int ex = v > g.clip_limit ? v - g.clip_limit : 0;
     v = v > g.clip_limit ? g.clip_limit : v;
@@ -185,6 +213,7 @@ __device__ __forceinline__ void clahe_lut_body(const uint8_t* __restrict__ in,
   } else {
     dst[t] = (uint8_t)sat_u8(__float2int_rn(f));
   }
+  return true;
 }
 
 template <int SPACE>
@@ -934,10 +963,14 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
 constexpr int kPrepMaxTiles = 64;
 constexpr int kPrepCtr0 = 16;  // ctr: [0, 8) queue heads, [8] timeout flag, then B x tiles rows
 
+constexpr int kPrepSlices = 4;  // workgroups per tile histogram
+constexpr int kPrepAhead = 2;   // LUT rows queued ahead of the blocks that wait on them
+
 struct PrepQueue {
-  int tiles, ntx, per_frame, B;
+  int tiles, ntx, per_frame, B, ahead;
   int rows_end[kPrepMaxTiles];  // block rows whose LUT rows are all <= k (a prefix)
-  int* ctr;
+  int* ctr;                     // queue heads, flag, B x tiles row counters, B x tiles^2 tile counters
+  int* part;                    // B x tiles^2 x kPrepSlices x 256 partial histograms
 };
 
 // threadIdx.x through a volatile move: the item bodies' thread-constant
@@ -992,22 +1025,39 @@ __global__ __launch_bounds__(256) void prep_oneread_kernel(const uint8_t* __rest
       const int fl = it / Q.per_frame;
       const int b = q + 8 * fl;
       int r = it - fl * Q.per_frame;
+      // a frame's items: the slices of LUT rows 0 .. ahead-1, then per k the
+      // slices of LUT row k + ahead and the blocks whose rows are all <= k
+      const int TS = Q.tiles * kPrepSlices;
       bool is_lut = false;
-      int idx = 0, jb0 = 0;
-      for (int k = 0; k < Q.tiles; ++k) {
-        if (r < Q.tiles) {
-          is_lut = true;
-          idx = k * Q.tiles + r;
-          break;
+      int idx = 0, jb0 = 0, lrow = 0;
+      if (r < Q.ahead * TS) {
+        is_lut = true;
+        lrow = r / TS;
+        r -= lrow * TS;
+      } else {
+        r -= Q.ahead * TS;
+        for (int k = 0; k < Q.tiles; ++k) {
+          if (k + Q.ahead < Q.tiles) {
+            if (r < TS) {
+              is_lut = true;
+              lrow = k + Q.ahead;
+              break;
+            }
+            r -= TS;
+          }
+          const int nb = (Q.rows_end[k] - jb0) * Q.ntx;
+          if (r < nb) {
+            idx = jb0 * Q.ntx + r;
+            break;
+          }
+          r -= nb;
+          jb0 = Q.rows_end[k];
         }
-        r -= Q.tiles;
-        const int nb = (Q.rows_end[k] - jb0) * Q.ntx;
-        if (r < nb) {
-          idx = jb0 * Q.ntx + r;
-          break;
-        }
-        r -= nb;
-        jb0 = Q.rows_end[k];
+      }
+      int slice = 0;
+      if (is_lut) {  // r: slice item within the row, tile-major
+        idx = lrow * Q.tiles + r / kPrepSlices;
+        slice = r - (r / kPrepSlices) * kPrepSlices;
       }
       int* rows = Q.ctr + kPrepCtr0 + b * Q.tiles;
       if (!is_lut) {
@@ -1044,11 +1094,21 @@ __global__ __launch_bounds__(256) void prep_oneread_kernel(const uint8_t* __rest
       int nxt = 0;
       if (tid == 0) nxt = atomicAdd(&Q.ctr[q], 1);
       if (is_lut) {
-        clahe_lut_body<kYCrCb, true>(in, lut, H, W, pitch, g, idx, b, opaque_tid());
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0)
-          __hip_atomic_fetch_add(rows + idx / Q.tiles, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int hs = (g.th + kPrepSlices - 1) / kPrepSlices;
+        const int tt = b * Q.tiles * Q.tiles + idx;
+        LutSlice sl;
+        sl.r_lo = min(slice * hs, g.th);
+        sl.r_hi = min(sl.r_lo + hs, g.th);
+        sl.slice = slice;
+        sl.nslice = kPrepSlices;
+        sl.part = Q.part + (size_t)tt * kPrepSlices * 256;
+        sl.tile_ctr = Q.ctr + kPrepCtr0 + Q.B * Q.tiles + tt;
+        if (clahe_lut_body<kYCrCb, true>(in, lut, H, W, pitch, g, idx, b, opaque_tid(), &sl)) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (tid == 0)
+            __hip_atomic_fetch_add(rows + idx / Q.tiles, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       } else {
         const int by = idx / Q.ntx, bx = idx - by * Q.ntx;
         med3_body<true, LB, true>(in, out, lut, H, W, pitch, vec, g, lb, b, bx * kM3W, by * kM3H,
@@ -1062,14 +1122,20 @@ __global__ __launch_bounds__(256) void prep_oneread_kernel(const uint8_t* __rest
   }
 }
 
-static bool prep_queue(const ClaheGeo& g, int H, int W, int B, int* ctr, PrepQueue& Q) {
+static size_t lut_bytes(int B, int tiles) { return (size_t)B * tiles * tiles * 256; }
+static size_t prep_ctr_ints(int B, int tiles) { return kPrepCtr0 + (size_t)B * tiles * (1 + tiles); }
+static size_t prep_ctr_bytes(int B, int tiles) { return (prep_ctr_ints(B, tiles) * 4 + 255) & ~(size_t)255; }
+
+static bool prep_queue(const ClaheGeo& g, int H, int W, int B, uint8_t* ws, PrepQueue& Q) {
   if (g.tiles > kPrepMaxTiles) return false;
   Q.tiles = g.tiles;
   Q.ntx = ceil_div(W, kM3W);
   const int nty = ceil_div(H, kM3H);
-  Q.per_frame = g.tiles * g.tiles + Q.ntx * nty;
+  Q.per_frame = g.tiles * g.tiles * kPrepSlices + Q.ntx * nty;
   Q.B = B;
-  Q.ctr = ctr;
+  Q.ahead = std::min(kPrepAhead, g.tiles);
+  Q.ctr = (int*)(ws + lut_bytes(B, g.tiles));
+  Q.part = (int*)(ws + lut_bytes(B, g.tiles) + prep_ctr_bytes(B, g.tiles));
   for (int k = 0; k < kPrepMaxTiles; ++k) {
     int n = 0;
     while (n < nty && prep_row_hi(n * kM3H, H, g.th, g.tiles) <= k) ++n;
@@ -1087,8 +1153,6 @@ static bool prep_oneread_on() {
   const char* e = getenv("RV_PREP_ONEREAD");
   return e && atoi(e) != 0;
 }
-
-static size_t lut_bytes(int B, int tiles) { return (size_t)B * tiles * tiles * 256; }
 
 // Host checks for med3_kernel.
 // Upper bound of ncx * ncy in the kernel: distinct floor(p/t - 0.5) over a
@@ -1204,10 +1268,12 @@ static int check_frames(const uint8_t* in, const void* out, int B, int H, int W,
   return RV_OK;
 }
 
-// B x tiles^2 LUTs, then the single-read pass's queue and row counters
+// B x tiles^2 LUTs, then the single-read pass's counters and partial
+// histograms (RV_PREP_ONEREAD=1)
 extern "C" size_t rv_clahe_ws_bytes(int B, int tiles) {
   if (B <= 0 || tiles <= 0) return 0;
-  return lut_bytes(B, tiles) + (((size_t)(kPrepCtr0 + B * tiles) * 4 + 255) & ~(size_t)255);
+  return lut_bytes(B, tiles) + prep_ctr_bytes(B, tiles) +
+         (size_t)B * tiles * tiles * kPrepSlices * 256 * 4;
 }
 
 extern "C" int rv_clahe_ycrcb_u8(const uint8_t* in, uint8_t* out, int B, int H, int W, int pitch,
@@ -1353,8 +1419,7 @@ extern "C" int rv_clahe_median_letterbox_u8(const uint8_t* in, uint8_t* out, int
   st = launch_letterbox_pad(lb_out, B, lb.g, s);
   if (st) return st;
   PrepQueue Q;
-  int* ctr = (int*)(lut + lut_bytes(B, tiles));
-  if (prep_oneread_on() && prep_queue(g, H, W, B, ctr, Q)) {
+  if (prep_oneread_on() && prep_queue(g, H, W, B, lut, Q)) {
     const int vec = (pitch % 4 == 0) && (((uintptr_t)in) % 4 == 0) && (((uintptr_t)out) % 4 == 0);
     const size_t cell_bytes = (size_t)med3_cells(g) * 1024;
     static int occ = 0;
@@ -1368,10 +1433,11 @@ extern "C" int rv_clahe_median_letterbox_u8(const uint8_t* in, uint8_t* out, int
     if (hipGetDevice(&dev) == hipSuccess)
       (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipGetLastError();
-    hipError_t e = hipMemsetAsync(ctr, 0, (size_t)(kPrepCtr0 + B * tiles) * 4, s);
+    hipError_t e = hipMemsetAsync(Q.ctr, 0, prep_ctr_ints(B, tiles) * 4, s);
     if (e != hipSuccess) return launch_status("rv_clahe_median_letterbox_u8 (memset)");
     const int items = B * Q.per_frame;
-    const int grid = std::min(items, std::max(8, ncu * occ));
+    const char* wg = getenv("RV_PREP_WGS");  // A/B probe: workgroups of the persistent grid
+    const int grid = std::min(items, std::max(8, wg ? atoi(wg) : ncu * occ));
     prep_oneread_kernel<true><<<grid, 256, cell_bytes, s>>>(in, out, lut, H, W, pitch, vec, g, lb, Q);
     return launch_status("rv_clahe_median_letterbox_u8");
   }
