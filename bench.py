@@ -88,7 +88,7 @@ def parse_args(argv=None):
                          "'ramp' (units of 1 and 2 steps at both ends of the run, pair steps "
                          "between: a shorter pipeline fill and drain), or an explicit "
                          "comma-separated list summing to --steps")
-    ap.add_argument("--warm-runs", type=int, default=int(os.environ.get("RV_WARM_RUNS", 1)),
+    ap.add_argument("--warm-runs", type=int, default=int(os.environ.get("RV_WARM_RUNS", 3)),
                     help="untimed runs of the recorded schedule over the timed frames before the "
                          "timed region (warm-up of the schedule itself)")
     ap.add_argument("--no-consumer", action="store_true",
