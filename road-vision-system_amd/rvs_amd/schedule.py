@@ -227,6 +227,13 @@ class PipelinedRun:
         import os
         if os.environ.get("RV_PREP_PRIORITY"):  # A/B probe: the preprocess stream's priority
             self.sp = torch.cuda.Stream(dev, priority=int(os.environ["RV_PREP_PRIORITY"]))
+        # A/B probe: RV_HIPRI_STREAMS=sy,sm,st creates those stage streams at
+        # high priority (torch: -1), e.g. the later stages ahead of the next
+        # units' preprocess during the pipeline fill
+        for name in filter(None, os.environ.get("RV_HIPRI_STREAMS", "").split(",")):
+            if name not in ("sm", "sp", "sy", "st"):
+                raise ValueError(f"RV_HIPRI_STREAMS: unknown stream {name!r}")
+            setattr(self, name, torch.cuda.Stream(dev, priority=-1))
         # RV_TRACK_ON_Y2=1: the track stage T(u) runs on the second-half
         # stream right behind Y2(u) (its only producer), one stream fewer
         # competing for the process's hardware queues
