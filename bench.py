@@ -112,6 +112,9 @@ def parse_args(argv=None):
                     help="CPU baseline workers (0: OMP_NUM_THREADS, else the CPUs this process "
                          "may run on)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the pair-1 rate and the secondary legs (configs[1], configs[4], "
+                         "host-fed NV12; bench_extra.py)")
     ap.add_argument("--job", default=None,
                     help="module:Class of a stand-in rank job (CPU rehearsal of the rank logic "
                          "with gloo; tests/test_shard_gloo.py)")
@@ -175,7 +178,7 @@ def spawn_ranks(n: int, argv) -> int:
 class BenchJob:
     """What one rank runs: its 32 camera streams through the full chain."""
 
-    def __init__(self, args, rank: int, dev):
+    def __init__(self, args, rank: int, dev, frames=None):
         from rvs_amd.engine import RoadVisionEngine
         from rvs_amd.shard import rank_streams
         from rvs_amd.synth import road_frames
@@ -187,8 +190,8 @@ class BenchJob:
         lanes, pair = (1, 1) if seq else (2, max(self.unit_sizes))
         self.eng = RoadVisionEngine(self.cfg, self.S, (H, W), device=dev, tmax=args.tmax,
                                     lanes=lanes, pair=pair)
-        self.frames = road_frames(self.S, self.Wm + self.K, H, W, device=dev,
-                                  stream_offset=rank_streams(self.S, rank).start)
+        self.frames = frames if frames is not None else road_frames(
+            self.S, self.Wm + self.K, H, W, device=dev, stream_offset=rank_streams(self.S, rank).start)
         self.ts = torch.tensor([[f / 30.0] * self.S for f in range(self.Wm + self.K)],
                                dtype=torch.float64, device=dev)
         self.units = self.S * self.K
@@ -201,6 +204,8 @@ class BenchJob:
         self.records = None
         self.device_end = 0.0
         self.issue_s = 0.0
+        self.tags = (1, 2)       # rv_trace_marker tags around the timed region
+        self.sort_saved = None   # SORT state the timed region starts from
         torch.cuda.synchronize()
 
     def warmup(self):
@@ -237,13 +242,13 @@ class BenchJob:
                                        [self.ts[Wm + k] for k in range(K)], mode=a.exec_mode,
                                        sync=a.sync, units=self.unit_sizes)
             self.records = self.runner.records
-            if a.warm_runs > 0:
-                # the SORT state is restored afterwards, so the timed run sees
-                # exactly the tracks the warm-up steps left
-                saved = eng.tracker.state[0].clone()
-                for _ in range(a.warm_runs):
-                    self.runner.run()
-                eng.tracker.state[0].copy_(saved)
+            # the SORT state is restored after the warm runs (and before the
+            # device-only rerun), so every timed run sees exactly the tracks
+            # the warm-up steps left
+            self.sort_saved = eng.tracker.state[0].clone()
+            for _ in range(a.warm_runs):
+                self.runner.run()
+            eng.tracker.state[0].copy_(self.sort_saved)
         torch.cuda.synchronize()
 
     def _consume(self, wait_step, materialise: bool):
@@ -276,7 +281,7 @@ class BenchJob:
     def run(self):
         from rvs_amd import _lib
         st = _lib.stream_ptr()
-        _lib.call("rv_trace_marker", 1, st)  # brackets the timed region in a kernel trace
+        _lib.call("rv_trace_marker", self.tags[0], st)  # brackets the region in a kernel trace
         t0 = time.perf_counter()
         if self.runner is not None:
             self.runner.run()
@@ -290,7 +295,7 @@ class BenchJob:
                 evs.append(e)
             wait = lambda k: evs[k].synchronize()  # noqa: E731
         self.issue_s = time.perf_counter() - t0
-        _lib.call("rv_trace_marker", 2, st)
+        _lib.call("rv_trace_marker", self.tags[1], st)
         if self.consume != "off":
             self._consumer = threading.Thread(target=self._consume,
                                               args=(wait, self.consume == "consume"))
@@ -321,31 +326,54 @@ def rank_job(job, device) -> dict:
 
 def rank_job_again(job, device) -> dict:
     """A second timed region over the same recorded schedule, without the
-    Detection lists (a watcher thread only notes each step's completion)."""
+    Detection lists (a watcher thread only notes each step's completion),
+    from the same SORT state as the first (the same timestamps replayed on
+    continued tracks would run time backwards), bracketed by marker tags 7/8."""
     from rvs_amd.shard import timed_job
     consume, job.consume = job.consume, "watch"
+    tags, job.tags = job.tags, (7, 8)
+    if job.sort_saved is not None:
+        job.eng.tracker.state[0].copy_(job.sort_saved)
     try:
         return timed_job(job.run, job.sync, job.units, device)
     finally:
         job.consume = consume
+        job.tags = tags
+
+
+def _union_ms(t0, t1) -> float:
+    """Total length of the union of the intervals [t0[i], t1[i])."""
+    tot, cs, ce = 0.0, None, None
+    for a, b in sorted(zip(t0, t1)):
+        if ce is None or a > ce:
+            if ce is not None:
+                tot += ce - cs
+            cs, ce = a, b
+        else:
+            ce = max(ce, b)
+    return tot + (ce - cs if ce is not None else 0.0)
 
 
 def _conv_pass(job, mode: str, tags):
     """One profiled pass over the K steps: HIP events around every conv
-    launch of lane 0's forwards (rv_yolo_profile), bracketed by trace
-    markers `tags` so tools/trace_window.py can cut the same window out of
-    a rocprofv3 trace.  Returns (ms per step, FLOPs, bytes, launches)."""
+    launch of every forward context (rv_yolo_profile on each lane's handle),
+    bracketed by trace markers `tags` so tools/trace_window.py can cut the
+    same window out of a rocprofv3 trace.  Returns per step: (summed launch
+    ms, FLOPs, bytes, launches, chip-union ms of the conv launches)."""
     from rvs_amd import _lib
     from rvs_amd.schedule import PipelinedRun
     eng, K, Wm = job.eng, job.K, job.Wm
     lib = _lib.load()
-    h = eng.detector._h
+    hs = list(eng.detector._hs)
     # eager: each conv launched 5x back to back between its events, so an
     # event pair times kernels, not the dispatch gap in front of one kernel
-    _lib.check(lib.rv_yolo_profile_reps(h, K, 5 if mode == "eager" else 1), "rv_yolo_profile")
+    for h in hs:
+        _lib.check(lib.rv_yolo_profile_reps(h, K, 5 if mode == "eager" else 1), "rv_yolo_profile")
     st = _lib.stream_ptr()
     _lib.call("rv_trace_marker", tags[0], st)
     if mode == "overlap":  # the timed region's schedule, issued eagerly with the events
+        if job.sort_saved is not None:
+            eng.tracker.state[0].copy_(job.sort_saved)
         prof = PipelinedRun(eng, [job.frames[Wm + k] for k in range(K)],
                             [job.ts[Wm + k] for k in range(K)], mode="eager", sync=job.args.sync,
                             units=job.unit_sizes)
@@ -363,27 +391,44 @@ def _conv_pass(job, mode: str, tags):
     _lib.call("rv_trace_marker", tags[1], st)
     torch.cuda.synchronize()
     n = lib.rv_yolo_num_convs(eng.variant)
-    ms, fl, by = np.zeros(n), np.zeros(n), np.zeros(n)
-    cv = np.zeros(n, np.int32)
-    nf = lib.rv_yolo_profile_read(h, ms.ctypes.data, fl.ctypes.data, cv.ctypes.data, n)
-    lib.rv_yolo_profile_bytes(h, by.ctypes.data, n)
+    ms_tot, nf_tot = np.zeros(n), 0
+    fl, by, cv = np.zeros(n), np.zeros(n), np.zeros(n, np.int32)
+    t0s, t1s = [], []
+    for h in hs:
+        ms = np.zeros(n)
+        nf = lib.rv_yolo_profile_read(h, ms.ctypes.data, fl.ctypes.data, cv.ctypes.data, n)
+        if nf <= 0:
+            continue
+        lib.rv_yolo_profile_bytes(h, by.ctypes.data, n)
+        ms_tot += ms
+        nf_tot += nf
+        cnt = lib.rv_yolo_profile_times(h, hs[0], None, None, 0) \
+            if hasattr(lib, "rv_yolo_profile_times") else 0  # (an older A/B build lacks it)
+        if cnt > 0:
+            a, b = np.zeros(cnt), np.zeros(cnt)
+            lib.rv_yolo_profile_times(h, hs[0], a.ctypes.data, b.ctypes.data, cnt)
+            t0s += a.tolist()
+            t1s += b.tolist()
     torch.cuda.synchronize()
-    lib.rv_yolo_profile(h, 0)
+    for h in hs:
+        lib.rv_yolo_profile(h, 0)
     valid = cv >= 0
+    # every profiled forward covers `pair` steps -> per step
+    per = eng.pair
+    steps = max(nf_tot, 1) * per
+    union = _union_ms(t0s, t1s) / steps if mode == "overlap" else None
     table = os.environ.get("RV_CONV_TABLE")
     if table:  # per-launch table of this pass (tools: per-layer roofline)
         from rvs_amd.detect.weights import conv_list
         names = [c[0] for c in conv_list(eng.variant)]
         names[0] = "stem (model.0 + model.1 + model.2.cv1)"  # slot n - 1: the fused stem
         with open(f"{table}_{mode}.json", "w") as f:
-            json.dump({"mode": mode, "forwards": int(nf), "batch": eng.S * eng.pair,
-                       "launches": [{"conv": names[int(cv[i])], "us": ms[i] / max(nf, 1) * 1e3,
+            json.dump({"mode": mode, "forwards": int(nf_tot), "batch": eng.S * eng.pair,
+                       "launches": [{"conv": names[int(cv[i])], "us": ms_tot[i] / max(nf_tot, 1) * 1e3,
                                      "gflop": fl[i] / 1e9, "mb": by[i] / 1e6}
                                     for i in range(n) if cv[i] >= 0]}, f, indent=0)
-    # every profiled forward covers `pair` steps -> per step
-    per = eng.pair
-    return (float(ms[valid].sum()) / max(nf, 1) / per, float(fl[valid].sum()) / per,
-            float(by[valid].sum()) / per, int(valid.sum()) / per)
+    return (float(ms_tot[valid].sum()) / steps, float(fl[valid].sum()) / per,
+            float(by[valid].sum()) / per, int(valid.sum()) / per, union)
 
 
 def _lib_sha256() -> str:
@@ -418,10 +463,14 @@ def conv_roofline(job, mode: str) -> dict:
       "eager": one pipeline unit at a time, each launch alone, five times
                back to back between its events -- the kernels' own speed
                (the headline; rocprofv3 cross-check: trace window between
-               the 5th and 6th rv_trace_marker);
-      "overlap": the timed region's schedule issued eagerly, so each launch
-               sees the concurrency it has in the timed region
-               (`in_pipeline`; window: markers 3 and 4).
+               the rv_trace_marker tags 5 and 6);
+      "overlap": the timed region's schedule issued eagerly (tags 3 and 4),
+               so each launch sees the concurrency it has in the timed
+               region (`in_pipeline`): achieved = FLOPs / the chip-union
+               busy time of the conv launches of both forward lanes (the
+               time at least one conv launch is in flight), which can never
+               exceed the step time; the summed launch durations (2-3
+               streams run conv launches at once) are reported beside it.
     The bytes view (algorithmic activation + weight bytes of the launches at
     8 TB/s) is reported beside it."""
     job.runner = None
@@ -431,31 +480,38 @@ def conv_roofline(job, mode: str) -> dict:
         if mode in (m, "both"):
             res[m] = _conv_pass(job, m, tags)
 
-    def view(conv_ms, flop, byts, nl):
-        tflops = flop / (conv_ms * 1e-3) / 1e12
-        gbs = byts / (conv_ms * 1e-3) / 1e9
-        return {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16,
-                "unit": "TFLOP/s", "frac": round(tflops / PEAK_BF16, 5),
-                "bytes_view": {"achieved_gbs": round(gbs, 1), "peak_gbs": PEAK_HBM,
-                               "frac": round(gbs / PEAK_HBM, 5),
-                               "algorithmic_bytes_per_step": round(byts)},
-                "launches_per_step": nl, "conv_ms_per_step": round(conv_ms, 4),
-                "algorithmic_gflop_per_step": round(flop / 1e9, 2)}
+    def view(conv_ms, flop, byts, nl, union=None):
+        t = union if union else conv_ms
+        tflops = flop / (t * 1e-3) / 1e12
+        gbs = byts / (t * 1e-3) / 1e9
+        v = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16,
+             "unit": "TFLOP/s", "frac": round(tflops / PEAK_BF16, 5),
+             "bytes_view": {"achieved_gbs": round(gbs, 1), "peak_gbs": PEAK_HBM,
+                            "frac": round(gbs / PEAK_HBM, 5),
+                            "algorithmic_bytes_per_step": round(byts)},
+             "launches_per_step": nl, "conv_ms_per_step": round(t, 4),
+             "algorithmic_gflop_per_step": round(flop / 1e9, 2)}
+        if union:
+            v["summed_launch_ms_per_step"] = round(conv_ms, 4)
+        return v
     if not res or any(v[0] <= 0 for v in res.values()):
         return {"error": "no event timings"}
     main = "eager" if "eager" in res else "overlap"
     out = {"kernel": "conv family: conv_patch_kernel + conv1x1_direct_kernel + c2f_chain_kernel "
                      "+ stem_kernel "
                      "(all YOLOv8n conv launches of a step; HIP events on the launch stream)",
-           "timing": main + (" (one pipeline unit at a time: each launch alone, on the timed "
-                             "region's forward batch)" if main == "eager" else
-                             " (the timed region's schedule issued eagerly)")}
+           "timing": main + (" (one pipeline unit at a time: each launch alone, 5 back-to-back "
+                             "repetitions between its events, on the timed region's forward "
+                             "batch; trace window: marker tags 5-6)" if main == "eager" else
+                             " (the timed region's schedule issued eagerly; chip-union busy time)")}
     out.update(view(*res[main]))
     out.update(pmc_traffic())
     if main == "eager" and "overlap" in res:
         out["in_pipeline"] = dict(view(*res["overlap"]), timing=(
-            "the timed region's schedule issued eagerly: each conv launch timed under the "
-            "concurrency it has in the timed region"))
+            "the timed region's schedule issued eagerly (trace window: marker tags 3-4): "
+            "conv_ms_per_step = the chip-union busy time of the conv launches of both forward "
+            "lanes (HIP events on each launch stream), summed_launch_ms_per_step = their summed "
+            "durations"))
     return out
 
 
@@ -568,18 +624,74 @@ def steady_state(job) -> dict:
                                    "device-only run (host clock, watcher thread)"}
 
 
+def _cpu_baseline_leg(args, rank: int, world: int, cfg) -> dict:
+    """The CPU baseline, on rank 0 only, after the ranks' last barrier (the
+    other ranks are done with the GPU by then): at N > 1 the scaling line
+    keeps its baseline too.  {} when disabled or not rank 0."""
+    if rank != 0 or args.no_cpu_baseline or args.cpu_frames <= 0:
+        return {}
+    workers = args.cpu_workers or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or \
+        len(os.sched_getaffinity(0))
+    return {"cpu_baseline": cpu_baseline(cfg, args.cpu_frames, workers)}
+
+
+def _rank_fields(t: dict, world: int) -> dict:
+    return {"world_size": torch.distributed.get_world_size()
+            if torch.distributed.is_initialized() else 1,
+            "per_rank_local_s": [round(x, 6) for x in t["per_rank_s"]],
+            "local_s": round(t["local_s"], 6), "elapsed_s": round(t["elapsed_s"], 6)}
+
+
 def _stub_main(args, rank, world) -> None:
     """Rank logic with a stand-in job (CPU rehearsal with gloo)."""
     mod, cls = args.job.split(":")
     job = getattr(importlib.import_module(mod), cls)(args, rank, "cpu")
     t = rank_job(job, "cpu")
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": t["value"], "unit": "frames/s",
-                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": t["elapsed_s"] / args.steps * 1e3,
-                          "world_size": torch.distributed.get_world_size()
-                          if torch.distributed.is_initialized() else 1,
-                          "local_s": t["local_s"], "elapsed_s": t["elapsed_s"]}), flush=True)
+        res = {"metric": METRIC, "value": t["value"], "unit": "frames/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": t["elapsed_s"] / args.steps * 1e3}
+        res.update(_rank_fields(t, world))
+        res.update(_cpu_baseline_leg(args, rank, world, bench_config()))
+        print(json.dumps(res), flush=True)
+
+
+def pair1_rate(job, rank: int, dev) -> dict:
+    """The config's literal batch: one YOLOv8n forward per 32-stream step
+    (pipeline units of 1 step, autotuned at batch 32, the same K steps and
+    frames, the Detection consumer on), timed like the headline."""
+    from rvs_amd.shard import timed_job
+    a = argparse.Namespace(**vars(job.args))
+    a.pair, a.units, a.warm_runs, a.tune_load, a.tune_save = 1, "even", 1, None, None
+    j1 = BenchJob(a, rank, dev, frames=job.frames)
+    j1.warmup()
+    j1.prepare()
+    t = timed_job(j1.run, j1.sync, j1.units, dev)
+    j1.eng.close()
+    return {"value": round(t["value"], 2), "ms_per_step": round(t["elapsed_s"] / j1.K * 1e3, 4),
+            "forward_batch": j1.S,
+            "note": "pipeline units of 1 step: one forward over the step's 32 frames (the "
+                    "config's batch=32), conv kernels autotuned at batch 32; same K steps, "
+                    "frames and consumer as the headline"}
+
+
+def secondary_legs(job, dev) -> dict:
+    """BASELINE configs[1] and configs[4], and the host-fed rate of
+    configs[2] (bench_extra.py): a few seconds each; errors are reported,
+    not raised (the headline stands on its own)."""
+    import bench_extra
+    out = {}
+    for key, fn in (("config2_b1_latency", lambda: bench_extra.config2_latency(dev)),
+                    ("config5_fp8", lambda: bench_extra.config5_fp8(dev)),
+                    ("hostfed_nv12", lambda: bench_extra.hostfed_nv12(job))):
+        t0 = time.perf_counter()
+        try:
+            out[key] = fn()
+        except Exception as e:  # noqa: BLE001 -- a failed leg must not hide the headline
+            out[key] = {"error": f"{type(e).__name__}: {e}"}
+        out[key]["leg_wall_s"] = round(time.perf_counter() - t0, 2)
+        torch.cuda.synchronize()
+    return out
 
 
 def main(argv=None):
@@ -598,16 +710,10 @@ def main(argv=None):
     torch.cuda.set_device(dev)
 
     job = BenchJob(args, rank, dev)
-    if os.environ.get("RV_BENCH_DEVICE_FIRST"):  # A/B probe: the device-only run first
-        job.warmup()
-        job.prepare()
-        rank_job_again(job, dev)
-        from rvs_amd.shard import timed_job
-        t = timed_job(job.run, job.sync, job.units, dev)
-    else:
-        t = rank_job(job, dev)
+    t = rank_job(job, dev)
     elapsed, value = t["elapsed_s"], t["value"]
     K, S = job.K, job.S
+    sort_rep = job.track_report()  # the tracks the timed region left
     cons = job.cons
     handback = {"consumer": ("in the timed region: a host thread builds every step's "
                              "List[Detection] per stream (rvs_amd.handback.Record.detections) as "
@@ -619,11 +725,10 @@ def main(argv=None):
         handback["detections_per_step"] = round(cons["detections"] / K, 1)
         handback["materialise_ms_per_step"] = round(cons["busy_s"] / K * 1e3, 3)
         handback["consumer_done_after_device_ms"] = round((cons["end"] - job.device_end) * 1e3, 3)
-    # the same K steps again without the consumer: the device-only rate, and
-    # the steady state from its per-step completion events
+    # the same K steps again without the consumer, from the same SORT state:
+    # the device-only rate, and the steady state from its per-step completions
     t2 = rank_job_again(job, dev) if job.consume == "consume" else None
     steady = steady_state(job)
-    sort_rep = job.track_report()
     roof = conv_roofline(job, args.conv_timing) if args.conv_timing != "none" else None
     P = job.eng.pair
     execution = ("sequential step() calls (no pipelining)" if args.exec_mode == "sequential" else
@@ -656,24 +761,30 @@ def main(argv=None):
                    "conv_autotune": ("loaded" if args.tune_load else (not args.no_autotune)),
                    "conv_grid": args.conv_grid,
                    "execution": execution},
-        "world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized()
-        else 1,
         "roofline": roof,
         "end_to_end_roofline_frac": round(value / world * (BYTES_PER_FRAME / (PEAK_HBM * 1e9) +
                                                            FLOP_PER_FRAME / (PEAK_BF16 * 1e12)), 5),
         "sort": sort_rep,
         "handback": handback,
     }
+    res.update(_rank_fields(t, world))
     if t2 is not None:
         res["device_only"] = {"value": round(t2["value"], 2),
                               "ms_per_step": round(t2["elapsed_s"] / K * 1e3, 4),
                               "note": "the same K steps timed again without the Detection "
-                                      "consumer (SORT continues from the first run)"}
+                                      "consumer, from the same SORT state (trace window: marker "
+                                      "tags 7-8)"}
     res.update(steady)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0:
-        workers = args.cpu_workers or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or \
-            len(os.sched_getaffinity(0))
-        res["cpu_baseline"] = cpu_baseline(job.cfg, args.cpu_frames, workers)
+    if world == 1 and not args.no_secondary:
+        if args.exec_mode != "sequential" and P > 1:
+            try:
+                res["pair1"] = pair1_rate(job, rank, dev)
+            except Exception as e:  # noqa: BLE001
+                res["pair1"] = {"error": f"{type(e).__name__}: {e}"}
+        res["secondary"] = secondary_legs(job, dev)
+    if world > 1:
+        torch.distributed.barrier()
+    res.update(_cpu_baseline_leg(args, rank, world, job.cfg))
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -254,6 +254,11 @@ int rv_yolo_profile_read(void* handle, double* ms, double* flops, int* conv, int
 /* Algorithmic HBM bytes of one launch per conv launch index (inputs read
  * once, outputs written, residual, weights); returns the entries written. */
 int rv_yolo_profile_bytes(void* handle, double* bytes, int n);
+/* [start, end) in ms of every recorded conv launch of `handle`, after the
+ * first recorded event of handle `ref` (same device clock), so the launches
+ * of several forward contexts merge into the conv family's chip-wide busy
+ * time.  Writes at most n pairs; returns the interval count. */
+int rv_yolo_profile_times(void* handle, void* ref, double* t0, double* t1, int n);
 
 /* Per-layer autotuning of the conv kernels (no reference counterpart: it
  * picks, per conv launch of this handle's forward, the fastest of the valid
@@ -518,9 +523,13 @@ int rv_sched_add_record(void* handle, void* stream, int timing, int* event);
 /* `stream` waits for event `event` (an earlier record node). */
 int rv_sched_add_wait(void* handle, void* stream, int event);
 int rv_sched_num_nodes(void* handle);
-/* Host wait (this thread only) for record node `event` of the last run. */
+/* Host wait (this thread only) for record node `event` of the last run.
+ * Valid only after rv_sched_run returned RV_OK for that run: RV_EINVAL
+ * before the first run, while a run is issuing, after a run that failed
+ * part-way, or for an event the latest run did not issue. */
 int rv_sched_event_sync(void* handle, int event);
-/* Milliseconds between two timing record nodes of the last run. */
+/* Milliseconds between two timing record nodes of the last run (same
+ * validity rule as rv_sched_event_sync). */
 int rv_sched_event_elapsed(void* handle, int a, int b, float* ms);
 /* Issue the whole schedule: every stream it uses waits for `origin`'s work
  * so far, the nodes are issued in record order, and `origin` waits for every

@@ -26,8 +26,11 @@ extern "C" const char* rv_last_error(void) { return rv::g_err; }
 // between them).  No reference counterpart: measurement plumbing only.
 __global__ void rv_trace_marker_kernel(int tag) { (void)tag; }
 
+// The marker's grid is `tag` workgroups of 64, so a kernel trace's
+// Grid_Size_X (= 64 * tag) names the tag (tools/trace_window.py).
 extern "C" int rv_trace_marker(int tag, void* stream) {
-  rv_trace_marker_kernel<<<1, 64, 0, rv::as_stream(stream)>>>(tag);
+  RV_CHECK_ARG(tag >= 1 && tag <= 64, "rv_trace_marker: tag %d outside [1, 64]", tag);
+  rv_trace_marker_kernel<<<tag, 64, 0, rv::as_stream(stream)>>>(tag);
   return rv::launch_status("rv_trace_marker");
 }
 

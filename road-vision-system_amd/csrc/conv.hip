@@ -304,6 +304,35 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------------
 __device__ __attribute__((aligned(64))) uint4 g_zero16[4];
 
+// XCD-aware pixel-tile walk.  Workgroups are dispatched to the 8 XCDs
+// round-robin by linear id, so with gridDim.x a multiple of 8 (the host
+// rounds it: xcd_grid) every cout tile blockIdx.y of blockIdx.x lands on
+// XCD blockIdx.x % 8.  XCD j then owns one contiguous run of pixel tiles
+// [j * chunk, (j + 1) * chunk) and its gridDim.x / 8 walkers step through it
+// together: the cout tiles of a pixel tile, and neighbouring tiles' shared
+// halo rows, are read from that XCD's L2 instead of being fetched into up
+// to 8 L2s (MI355X_MICROARCH.md: per-XCD L2s).  Other grids: plain stride.
+struct TileWalk {
+  int t0, step, end;
+  __device__ __forceinline__ int count() const { return t0 < end ? (end - t0 + step - 1) / step : 0; }
+};
+__device__ __forceinline__ TileWalk tile_walk(int ntiles) {
+  const int gx = gridDim.x, bx = blockIdx.x;
+  if ((gx & 7) == 0) {
+    const int chunk = (ntiles + 7) >> 3, j = bx & 7;
+    return TileWalk{j * chunk + (bx >> 3), gx >> 3, min(ntiles, (j + 1) * chunk)};
+  }
+  return TileWalk{bx, gx, ntiles};
+}
+// host side: a persistent grid of `want` walkers per cout tile, rounded down
+// to a multiple of 8 (at least 8 when there are that many tiles); a
+// one-block-per-tile grid rounded up (the surplus walkers get no tile)
+static inline int xcd_grid(int want, int ntiles, bool persist) {
+  if (!persist) return ntiles >= 8 ? (ntiles + 7) & ~7 : ntiles;
+  const int g = std::min(want, ntiles);
+  return g >= 8 ? g & ~7 : g;
+}
+
 // Buffer-resource LDS-DMA (conv_patch_kernel): dword3 of the descriptor
 // for a raw (stride 0) buffer on gfx950, and the voffset that the range
 // check (voffset + soffset against num_records, checked on the GPU:
@@ -623,8 +652,8 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
   constexpr int pad = K / 2;
   const int tiles_img = g.tiles_x * g.tiles_y;
   const int ntiles = a.B * tiles_img;
-  const int my_tiles = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int nsteps = my_tiles * ngrp;
+  const TileWalk walk = tile_walk(ntiles);
+  const int nsteps = walk.count() * ngrp;
   const int npp = g.PH * g.PW;
   const float inv_pw = 1.0f / (float)g.PW;
 
@@ -852,8 +881,8 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
   };
 
   if (nsteps == 0) return;
-  int ti = blockIdx.x;  // tile of the current step
-  int grp = 0;          // chunk group of the current step
+  int ti = walk.t0;  // tile of the current step
+  int grp = 0;       // chunk group of the current step
   if constexpr (RESW)
     for (int c = 0; c < nch; ++c) dma_weights(c, smem + c * W_BYTES);
   prep_tile(ti);
@@ -869,7 +898,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
     // issue step s+1
     const bool last = grp + 1 == ngrp;
     if (s + 1 < nsteps) {
-      if (last) prep_tile(ti + gridDim.x);
+      if (last) prep_tile(ti + walk.step);
       stage(last ? 0 : grp + 1, (s + 1) & 1);
     }
     compute(grp, s & 1);
@@ -896,7 +925,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
       } else {
         epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias);
       }
-      ti += gridDim.x;
+      ti += walk.step;
       grp = 0;
     } else {
       ++grp;
@@ -964,7 +993,11 @@ __global__ __launch_bounds__(256, 2) void conv1x1_direct_kernel(ConvArgs a, int 
     const int row = m * 16 + col;
     aoff[m] = row * 64 + ((quad ^ swzq<false>(row)) << 4);
   }
-  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  // (b, y, x) of a pixel only where it is used: the upsampled view and the
+  // generic epilogue (integer divisions are long VALU sequences)
+  const bool need_geo = a.in_up || !fast;
+  const TileWalk walk = tile_walk(ntiles);
+  for (int t = walk.t0; t < walk.end; t += walk.step) {
     const bf16_t* src[NR];
     const bf16_t* src2[NR];
     bool pv[NR];
@@ -974,10 +1007,13 @@ __global__ __launch_bounds__(256, 2) void conv1x1_direct_kernel(ConvArgs a, int 
       const int p = t * 64 * NR + wave * 16 * NR + n * 16 + col;
       pv[n] = p < npix;
       const int pp = pv[n] ? p : 0;
-      pb[n] = pp / HW;
-      const int r = pp - pb[n] * HW;
-      py[n] = r / a.Wo;
-      px[n] = r - py[n] * a.Wo;
+      pb[n] = py[n] = px[n] = 0;
+      if (need_geo) {
+        pb[n] = pp / HW;
+        const int r = pp - pb[n] * HW;
+        py[n] = r / a.Wo;
+        px[n] = r - py[n] * a.Wo;
+      }
       // the `in` view's pixel: itself, or (y/2, x/2) of the half-resolution map
       const size_t ps = a.in_up ? ((size_t)pb[n] * (a.Ho >> 1) + (py[n] >> 1)) * (a.Wo >> 1) + (px[n] >> 1)
                                 : (size_t)pp;
@@ -1135,8 +1171,7 @@ static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, int
   const int T = (a.Cout + 15) / 16;
   const int ytiles = ceil_div(T, MR);
   const int ntiles = a.B * g.tiles_x * g.tiles_y;
-  int gx = ntiles;
-  if (persist) gx = std::min(ntiles, std::max(1, num_cus() * occ / ytiles));
+  const int gx = xcd_grid(std::max(1, num_cus() * occ / ytiles), ntiles, persist != 0);
   dim3 grid(gx, ytiles);
   fn<<<grid, 256, smem, s>>>(a, g);
   return launch_status("conv_patch");
@@ -1180,8 +1215,7 @@ static int launch_direct_t(const ConvArgs& a, int persist, hipStream_t s) {
   }
   const int ytiles = ceil_div((a.Cout + 15) / 16, MR);
   const int ntiles = ceil_div(a.B * a.Ho * a.Wo, 64 * NR);
-  int gx = ntiles;
-  if (persist) gx = std::min(ntiles, std::max(1, num_cus() * occ / ytiles));
+  const int gx = xcd_grid(std::max(1, num_cus() * occ / ytiles), ntiles, persist != 0);
   fn<<<dim3(gx, ytiles), 256, smem, s>>>(a, epi_fast(a) ? 1 : 0);
   return launch_status("conv1x1_direct");
 }
@@ -1407,8 +1441,9 @@ static int try_launch_patch(const ConvArgs& a, hipStream_t s, int* st) {
 // |V| (yolo.hip pack_conv0q) in three balanced base-256 i8 digits, one MFMA
 // each, the accumulator started at 128 sum_k D_i[k] so it ends at
 // T_i = sum_k D_i[k] x[k] exactly (< 2^24, exact in f32).  The value is
-// s (65536 T0 + 256 T1 + T2) + b in f32 -- the f64 reference within 1 bf16
-// ulp (test_first_conv_sppf_and_decode).
+// s (65536 T0 + (256 T1 + T2)) + b in f32, with 256 T1 + T2 summed exactly in
+// i32 (|T_i| <= 27 * 128 * 255 < 2^20) and one fma -- the f64 reference within
+// 1 bf16 ulp (test_first_conv_sppf_and_decode).
 // Out-of-image window bytes read zeros through the buffer range check
 // (voffset kOOB), i.e. the zero padding of the normalised image.
 // ---------------------------------------------------------------------------
@@ -1475,7 +1510,7 @@ __device__ __forceinline__ void conv0_frag(const C0Wts<MR>& W, const i32x4 X, f3
     for (int i = 0; i < 3; ++i) t[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(W.d[m][i], X, W.c[m][i], 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float u = fmaf((float)t[0][i], 65536.0f, (float)t[1][i] * 256.0f) + (float)t[2][i];
+      const float u = fmaf((float)t[0][i], 65536.0f, (float)(t[1][i] * 256 + t[2][i]));
       v[m][i] = silu(fmaf(W.s[m][i], u, W.b[m][i]));
     }
   }
@@ -1569,14 +1604,21 @@ int launch_conv0_fp8(const uint8_t* img, int B, int H, int W, const Conv0Q& q, i
 //
 // X0 tile in LDS: 17 rows x (33 even + 32 odd columns) of 32-B pixels, the
 // even tile columns first, then the odd ones (stored column of tile column
-// xr: xr / 2, or 33 + xr / 2).  model.1 runs on "tap pairs": a 32-deep MFMA
-// k-step takes the 16 channels of two taps -- (kx 0, kx 1) = (even c, odd
-// c) for X1 column c, then (kx 2, phantom) = even c + 1 with zero weights
-// for the phantom -- so 16 consecutive X1 pixels read 16 consecutive 32-B
-// stored pixels of one region: every ds_read_b128 lane group hits 16
-// distinct 16-B bank slots (the interleaved image this replaces was 2-way
-// conflicted).  A fragments come from the standard packed weights
-// [Cout][ky][kx][32] and are held in registers for the whole kernel.
+// xr: xr / 2, or 33 + xr / 2), rows 72 stored pixels apart.  model.1 runs on
+// "tap pairs": a 32-deep MFMA k-step takes the 16 channels of two taps --
+// (kx 0, kx 1) = (even c, odd c) for X1 column c, then (kx 2, phantom) =
+// even c + 1 with zero weights for the phantom -- so 16 consecutive X1
+// pixels read 16 consecutive 32-B stored pixels of one region.
+// Swizzle: 16-B half h of stored pixel s sits at s * 32 + 16 (h ^ bit 2 of
+// s).  conv0 writes a pixel's half as one 16-B store (fragments f and f + 4
+// of a wave exchange their quad 0/1 and 2/3 channel quarters with
+// v_permlane16_swap first), and 8 consecutive pixels of a ds_write_b128 lane
+// group then cover all 32 banks; in model.1's ds_read_b128 lane groups the
+// 16 lanes hit 16 distinct 16-B bank slots for any row (72 = 0 mod 8 keeps
+// bit 2 per row).  (r03 stored 8-B quarters with ds_write_b64: 4-way
+// conflicts, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.57.)  A fragments
+// come from the standard packed weights [Cout][ky][kx][32] and are held in
+// registers for the whole kernel.
 //
 // With model.2.cv1 fused, model.1's output channels are computed in the
 // order that leaves lane quad q holding channels 8q .. 8q+7 of its pixel
@@ -1588,9 +1630,10 @@ int launch_conv0_fp8(const uint8_t* img, int B, int H, int W, const Conv0Q& q, i
 constexpr int kStR = 8, kStC = 32;           // X1 tile
 constexpr int kStXR = 2 * kStR + 1;          // X0 tile rows (17)
 constexpr int kStXE = kStC + 1;              // even X0 tile columns (33)
-constexpr int kStXW = 2 * kStC + 1;          // stored pixels per row (33 even + 32 odd)
-constexpr int kStRowB = kStXW * 32;          // 2080 B per X0 tile row
-constexpr int kStXB = kStXR * kStRowB;       // 35,360 B
+constexpr int kStXW = 2 * kStC + 1;          // X0 pixels per tile row (33 even + 32 odd)
+constexpr int kStXS = 72;                    // stored pixel slots per row (a multiple of 8)
+constexpr int kStRowB = kStXS * 32;          // 2304 B per X0 tile row
+constexpr int kStXB = kStXR * kStRowB;       // 39,168 B (4 blocks / CU)
 constexpr int kStNpx = kStXR * kStXW;        // 1105 X0 pixels per tile
 constexpr int kStNfr = (kStNpx + 15) / 16;   // 70 conv0 fragments
 
@@ -1618,36 +1661,63 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(img + (size_t)b * H * W * 3), 0, H * W * 3, kRsrcFlags);
 
-  // ---- 1. conv0 over the X0 tile, fragment f = stored pixels 16 f .. +15
+  // ---- 1. conv0 over the X0 tile: fragment f = tile pixels t = 16 f .. +15
+  //      (row t / 65, stored column t % 65); wave w runs the pairs (f, f + 4),
+  //      f = w + 8 i, and stores each pixel's 16-B halves (see the swizzle)
   {
     C0Wts<1> Wt;
     Wt.load(q0, 16, col, quad);
-    auto pix = [&](int f, int& Y, int& X, bool& ok) {
-      const int s = f * 16 + col;
-      const int yr = s / kStXW, j = s - (s / kStXW) * kStXW;
+    auto win = [&](int t, int yr, int j, bool& ok) {
       const int xr = j < kStXE ? 2 * j : 2 * (j - kStXE) + 1;
-      Y = xy0 + yr;
-      X = xx0 + xr;
-      ok = s < kStNpx && (unsigned)Y < (unsigned)H0 && (unsigned)X < (unsigned)W0;
+      const int Y = xy0 + yr, X = xx0 + xr;
+      ok = t < kStNpx && (unsigned)Y < (unsigned)H0 && (unsigned)X < (unsigned)W0;
+      return conv0_window(r, Y, X, quad, H, W * 3, ok);
     };
-    int Y, X;
-    bool ok;
-    pix(wave, Y, X, ok);
-    C0Win nxt = conv0_window(r, Y, X, quad, H, W * 3, ok);
-    for (int f = wave; f < kStNfr; f += 4) {
-      const C0Win cur = nxt;
-      const bool cok = ok;
-      if (f + 4 < kStNfr) {
-        pix(f + 4, Y, X, ok);
-        nxt = conv0_window(r, Y, X, quad, H, W * 3, ok);
+    // t += 128: 2 rows down, 2 stored columns left (65 = one row)
+    auto adv = [](int& yr, int& j) {
+      j -= 2;
+      yr += 2;
+      if (j < 0) {
+        j += kStXW;
+        yr -= 1;
       }
-      f32x4 v[1];
-      conv0_frag<1>(Wt, conv0_bop(cur), v);
+    };
+    int t = 16 * wave + col;
+    int ya = t / kStXW, ja = t - ya * kStXW;
+    int yb = (t + 64) / kStXW, jb = t + 64 - yb * kStXW;
+    const int npairs = (kStNfr - wave + 7) / 8;
+    bool oka, okb;
+    C0Win na = win(t, ya, ja, oka), nb = win(t + 64, yb, jb, okb);
+    for (int i = 0; i < npairs; ++i) {
+      const C0Win ca = na, cb = nb;
+      const bool cka = oka, ckb = okb;
+      // the pixel this lane stores: fragment f (quads 0, 2) or f + 4 (quads 1, 3)
+      const bool odd = quad & 1;
+      const int ts = odd ? t + 64 : t;
+      const int ss = (odd ? yb : ya) * kStXS + (odd ? jb : ja);
+      if (i + 1 < npairs) {
+        t += 128;
+        adv(ya, ja);
+        adv(yb, jb);
+        na = win(t, ya, ja, oka);
+        nb = win(t + 64, yb, jb, okb);
+      }
+      f32x4 va[1], vb[1];
+      conv0_frag<1>(Wt, conv0_bop(ca), va);
+      conv0_frag<1>(Wt, conv0_bop(cb), vb);
       // outside the X0 map the value is model.1's zero padding
-      const uint2 pk = cok ? make_uint2(pack_bf16x2(v[0][0], v[0][1]), pack_bf16x2(v[0][2], v[0][3]))
-                           : make_uint2(0, 0);
-      const int s = f * 16 + col;
-      if (s < kStNpx) *(uint2*)(xs + s * 32 + quad * 8) = pk;
+      uint32_t a0 = cka ? pack_bf16x2(va[0][0], va[0][1]) : 0u;
+      uint32_t a1 = cka ? pack_bf16x2(va[0][2], va[0][3]) : 0u;
+      uint32_t b0 = ckb ? pack_bf16x2(vb[0][0], vb[0][1]) : 0u;
+      uint32_t b1 = ckb ? pack_bf16x2(vb[0][2], vb[0][3]) : 0u;
+      // lanes 16-31 (48-63) of a <-> lanes 0-15 (32-47) of b: quad q then
+      // holds channels 8 (q >> 1) .. +7 of its pixel in (a0, a1, b0, b1)
+      const auto x0v = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+      const auto x1v = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+      if (ts < kStNpx) {
+        const int h = (quad >> 1) ^ ((ss >> 2) & 1);
+        *(uint4*)(xs + ss * 32 + h * 16) = make_uint4(x0v[0], x1v[0], x0v[1], x1v[1]);
+      }
     }
   }
   // model.1 A fragments (all 6 k-steps, L2-resident weights) while the
@@ -1677,14 +1747,16 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
     for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
   // this lane's B column: X1 pixel (row 2 wave + n / 2, col (n & 1) 16 + col)
   int bb0[NR], bb1[NR];
+  // byte address of half h of stored pixel s (the swizzle above)
+  auto xaddr = [](int s_, int h) { return s_ * 32 + ((h ^ ((s_ >> 2) & 1)) << 4); };
 #pragma unroll
   for (int n = 0; n < NR; ++n) {
     const int rr = 2 * wave + (n >> 1), c = (n & 1) * 16 + col;
-    const int rb = 2 * rr * kStRowB;
+    const int rs = 2 * rr * kStXS;
     // pair 0: quads 0,1 tap kx 0 (even c), quads 2,3 tap kx 1 (odd c)
-    bb0[n] = rb + (quad < 2 ? c * 32 + quad * 16 : (kStXE + c) * 32 + (quad - 2) * 16);
+    bb0[n] = quad < 2 ? xaddr(rs + c, quad) : xaddr(rs + kStXE + c, quad - 2);
     // pair 1: tap kx 2 (even c + 1); quads 2,3 (phantom tap) read the same
-    bb1[n] = rb + (c + 1) * 32 + (quad & 1) * 16;
+    bb1[n] = xaddr(rs + c + 1, quad & 1);
   }
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky)

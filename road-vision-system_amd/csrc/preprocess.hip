@@ -66,42 +66,28 @@ __device__ __forceinline__ int clahe_luma(int b, int g, int r) {
 
 // ---------------------------------------------------------------------------
 // Kernel A: per (tile, frame) histogram of Y -> clip -> redistribute -> LUT.
-// One 256-thread workgroup per tile.  16 LDS histogram copies (wave x lane
-// & 3), bin-major so the copies of one bin sit in 16 different banks: equal
-// Y values in a wave (flat sky / asphalt) spread over 4 addresses instead of
-// serialising on one, with no bank conflicts between the copies.  (One
-// copy per lane with packed u16 counters -- conflict-free for any Y -- was
-// measured slower: 47.5 vs 42.2 us at 32 x 1080p, the 33 KB of LDS halves
-// the resident blocks of this load-bound pass.)
+// One 256-thread workgroup per tile.  16 LDS histogram copies, copy = lane
+// & 15 (shared by the 4 waves), copy-major with a 257-word stride: bin y of
+// copy c is word 257 c + y, bank (c + y) mod 64.  Equal Y values in a wave
+// (flat sky / asphalt) land on 16 different banks, with at most 2 lanes of
+// a 32-lane group on one address (lanes l, l + 16); nearby Y values in
+// different copies spread over the banks as well.  (r02/r03 used copy =
+// wave x lane & 3, bin-major: one wave reached only 16 banks and up to 16
+// lanes hit one address -- SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.78.
+// One copy per lane with packed u16 counters was measured slower: 47.5 vs
+// 42.2 us at 32 x 1080p, its 33 KB of LDS halves the resident blocks.)
 // ---------------------------------------------------------------------------
-// SC1: the LUT is published to other workgroups of the same launch (the
-// single-read pass below): wave 0 stores it as 64 `sc1` dwords (each 128-B
-// line whole in one store instruction), the hand-off form of
-// MI355X_MICROARCH.md "Valid forms" (sc1 stores, agent counter, sc1 loads).
-// Slice mode (the single-read pass): the workgroup histograms tile rows
-// [r_lo, r_hi) only, stores that partial histogram (sc1) in `part` slot
-// `slice` of `nslice`, and the workgroup whose agent-scope add to the tile's
-// counter comes last sums the partials (sc1 loads) and builds the LUT.
-// Returns whether this workgroup built (and published) the LUT.
-struct LutSlice {
-  int r_lo, r_hi, slice, nslice;
-  int* part;      // nslice x 256 partial histograms of this tile
-  int* tile_ctr;  // slices finished for this tile
-};
-
-template <int SPACE, bool SC1>
-__device__ __forceinline__ bool clahe_lut_body(const uint8_t* __restrict__ in,
+template <int SPACE>
+__device__ __forceinline__ void clahe_lut_body(const uint8_t* __restrict__ in,
                                                uint8_t* __restrict__ lut, int H, int W, int pitch,
-                                               const ClaheGeo& g, int tile, int b, int t,
-                                               const LutSlice* sl = nullptr) {
+                                               const ClaheGeo& g, int tile, int b, int t) {
   constexpr int kCopies = 16;
-  constexpr int kWords = 256 * kCopies;
+  constexpr int kStride = 257;  // words per copy (odd: copy c shifts the banks by c)
+  constexpr int kWords = kStride * kCopies;
   __shared__ int hist[kWords];
   __shared__ int wsum[4], wtot[4];
-  __shared__ uint32_t lut_w[64];
-  __shared__ int s_last;
   const int wave = t >> 6;
-  const int r_lo = sl ? sl->r_lo : 0, r_hi = sl ? sl->r_hi : g.th;
+  const int r_lo = 0, r_hi = g.th;
   const int ty = tile / g.tiles, tx = tile - (tile / g.tiles) * g.tiles;
   const int x0 = tx * g.tw, y0 = ty * g.th;
   const uint8_t* frame = in + (size_t)b * H * pitch;
@@ -112,8 +98,8 @@ __device__ __forceinline__ bool clahe_lut_body(const uint8_t* __restrict__ in,
   const bool inside = (x0 + g.tw <= W) && (y0 + g.th <= H);
   const bool vec = inside && (g.tw % 4 == 0) && (pitch % 4 == 0) &&
                    ((((uintptr_t)frame) + (uintptr_t)x0 * 3) % 4 == 0);
-  int* h = hist + ((wave << 2) | (t & 3));  // bin y -> h[y * kCopies]
-  auto bump = [&](int y) { atomicAdd(&h[y * kCopies], 1); };
+  int* h = hist + (t & (kCopies - 1)) * kStride;  // bin y -> h[y]
+  auto bump = [&](int y) { atomicAdd(&h[y], 1); };
   if (vec) {
     const int groups = g.tw >> 2;
     const int total = groups * (r_hi - r_lo);
@@ -162,21 +148,7 @@ __device__ __forceinline__ bool clahe_lut_body(const uint8_t* __restrict__ in,
 
   int v = 0;
 #pragma unroll
-  for (int c = 0; c < kCopies; ++c) v += hist[t * kCopies + ((c + t) & (kCopies - 1))];
-  if (sl) {
-    // each wave stores 64 consecutive ints: two whole 128-B lines per store
-    __hip_atomic_store(sl->part + sl->slice * 256 + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0)
-      s_last = __hip_atomic_fetch_add(sl->tile_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-               sl->nslice - 1;
-    __syncthreads();
-    if (!s_last) return false;
-    v = 0;
-    for (int k = 0; k < sl->nslice; ++k)
-      v += __hip_atomic_load(sl->part + k * 256 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  for (int c = 0; c < kCopies; ++c) v += hist[c * kStride + t];
   if (g.clip_limit > 0) {
     int ex = v > g.clip_limit ? v - g.clip_limit : 0;
     v = v > g.clip_limit ? g.clip_limit : v;
@@ -205,22 +177,14 @@ __device__ __forceinline__ bool clahe_lut_body(const uint8_t* __restrict__ in,
   for (int w = 0; w < wave; ++w) v += wtot[w];
   const float f = (float)v * g.lut_scale;
   uint8_t* dst = lut + ((size_t)b * g.tiles * g.tiles + tile) * 256;
-  if constexpr (SC1) {
-    ((uint8_t*)lut_w)[t] = (uint8_t)sat_u8(__float2int_rn(f));
-    __syncthreads();
-    if (wave == 0)
-      __hip_atomic_store((uint32_t*)dst + t, lut_w[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    dst[t] = (uint8_t)sat_u8(__float2int_rn(f));
-  }
-  return true;
+  dst[t] = (uint8_t)sat_u8(__float2int_rn(f));
 }
 
 template <int SPACE>
 __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restrict__ in,
                                                         uint8_t* __restrict__ lut, int H, int W,
                                                         int pitch, ClaheGeo g) {
-  clahe_lut_body<SPACE, false>(in, lut, H, W, pitch, g, blockIdx.x, blockIdx.y, threadIdx.x);
+  clahe_lut_body<SPACE>(in, lut, H, W, pitch, g, blockIdx.x, blockIdx.y, threadIdx.x);
 }
 
 template <int SPACE>
@@ -634,9 +598,8 @@ __device__ __forceinline__ void clahe_ycc(int bb, int gg, int rr, const uint8_t*
   tr = dcr * (22987 * 4) + 8192 * 4;
 }
 
-// One 128 x 32 block (b, x0, y0).  SC1: the LUTs were published by other
-// workgroups of this launch and are read with `sc1` loads.
-template <bool CLAHE, bool LB, bool SC1>
+// One 128 x 32 block (b, x0, y0).
+template <bool CLAHE, bool LB>
 __device__ __forceinline__ void med3_body(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                           const uint8_t* __restrict__ lut, int H, int W, int pitch,
                                           int vec, const ClaheGeo& g, const LbFuse& lb, int b,
@@ -713,21 +676,10 @@ __device__ __forceinline__ void med3_body(const uint8_t* __restrict__ in, uint8_
       const int iy = cy0 + cy, ix = cx0 + cx;
       const int r1 = max(iy, 0), r2 = min(iy + 1, g.tiles - 1);
       const int c1 = max(ix, 0), c2 = min(ix + 1, g.tiles - 1);
-      uint32_t l11, l12, l21, l22;
-      if constexpr (SC1) {
-        auto ld = [&](int i) {
-          return __hip_atomic_load((uint32_t*)flut + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        };
-        l11 = ld((r1 * g.tiles + c1) * 64 + lane);
-        l12 = ld((r1 * g.tiles + c2) * 64 + lane);
-        l21 = ld((r2 * g.tiles + c1) * 64 + lane);
-        l22 = ld((r2 * g.tiles + c2) * 64 + lane);
-      } else {
-        l11 = flut[(r1 * g.tiles + c1) * 64 + lane];
-        l12 = flut[(r1 * g.tiles + c2) * 64 + lane];
-        l21 = flut[(r2 * g.tiles + c1) * 64 + lane];
-        l22 = flut[(r2 * g.tiles + c2) * 64 + lane];
-      }
+      const uint32_t l11 = flut[(r1 * g.tiles + c1) * 64 + lane];
+      const uint32_t l12 = flut[(r1 * g.tiles + c2) * 64 + lane];
+      const uint32_t l21 = flut[(r2 * g.tiles + c1) * 64 + lane];
+      const uint32_t l22 = flut[(r2 * g.tiles + c2) * 64 + lane];
       const uint32_t p_lo = __builtin_amdgcn_perm(l12, l11, 0x05010400u);  // a0 b0 a1 b1
       const uint32_t p_hi = __builtin_amdgcn_perm(l12, l11, 0x07030602u);  // a2 b2 a3 b3
       const uint32_t q_lo = __builtin_amdgcn_perm(l22, l21, 0x05010400u);
@@ -930,229 +882,11 @@ __global__ __launch_bounds__(256) void med3_kernel(const uint8_t* __restrict__ i
   const int t = xcd < r ? xcd * (q + 1) + slot : r * (q + 1) + (xcd - r) * q + slot;
   const int b = t / (ntx * nty);
   const int f = t - b * (ntx * nty);
-  med3_body<CLAHE, LB, false>(in, out, lut, H, W, pitch, vec, g, lb, b,
+  med3_body<CLAHE, LB>(in, out, lut, H, W, pitch, vec, g, lb, b,
                               (f - (f / ntx) * ntx) * kM3W, (f / ntx) * kM3H, threadIdx.x);
 }
 
-// ---------------------------------------------------------------------------
-// prep_oneread_kernel: the fused CLAHE + median + letterbox pass with ONE
-// read of every frame from HBM.  The two-launch form reads each 1080p frame
-// twice (the LUT pass, then the fused pass), and at 32 x 6.2 MB per step the
-// first read is long gone from every cache when the second comes.
-//
-// Here one persistent launch runs both kinds of work item from per-XCD
-// queues: frame b belongs to queue b % 8, and a frame's items are ordered so
-// every item depends only on earlier items of its own queue:
-//   LUT row 0 (tiles items: clahe_lut_body), LUT row 1, the 128 x 32 blocks
-//   whose LUT rows are all <= 1 (med3_body), LUT row 2, ...
-// A workgroup serves the queue of the XCD it runs on (HW_REG_XCC_ID), so a
-// tile row's pixels are read by the LUT item and re-read by its blocks a few
-// hundred microseconds later through the same 4 MiB L2; when its queue is
-// empty it helps the next queues (so no queue depends on the dispatcher's
-// XCD placement).
-// Hand-off of a LUT (MI355X_MICROARCH.md "Valid forms", first table row):
-// the LUT item's wave 0 stores the 256 B as sc1 dwords, every wave waits
-// vmcnt(0), a workgroup barrier, then one lane's agent-scope add to the
-// (frame, tile row) counter.  A block's lane 0 polls the counters of the
-// rows it blends with sc1 loads, a workgroup barrier, then every LUT load is
-// an sc1 load.  Deadlock freedom: a workgroup claims its next item only
-// after the wait of its current one, so a waiting block holds no other
-// item; everything it waits for was claimed earlier by running workgroups
-// whose LUT items never wait.  Every wait is bounded (a flag is raised).
-// ---------------------------------------------------------------------------
-constexpr int kPrepMaxTiles = 64;
-constexpr int kPrepCtr0 = 16;  // ctr: [0, 8) queue heads, [8] timeout flag, then B x tiles rows
-
-constexpr int kPrepSlices = 4;  // workgroups per tile histogram
-constexpr int kPrepAhead = 2;   // LUT rows queued ahead of the blocks that wait on them
-
-struct PrepQueue {
-  int tiles, ntx, per_frame, B, ahead;
-  int rows_end[kPrepMaxTiles];  // block rows whose LUT rows are all <= k (a prefix)
-  int* ctr;                     // queue heads, flag, B x tiles row counters, B x tiles^2 tile counters
-  int* part;                    // B x tiles^2 x kPrepSlices x 256 partial histograms
-};
-
-// threadIdx.x through a volatile move: the item bodies' thread-constant
-// values are recomputed per item instead of being hoisted out of the item
-// loop and held across it (125 -> ~85 VGPRs for the block body)
-__device__ __forceinline__ int opaque_tid() {
-  int t;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
-  return t;
-}
-
-__device__ __forceinline__ int xcc_id() {
-  // s_getreg_b32 HW_REG_XCC_ID (id 20), bits [3:0]
-  return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;
-}
-
-// tile rows a 128 x 32 block at y0 blends (conservative: cell row
-// floor(y / th - 0.5) of its halo rows and the one below)
-__host__ __device__ __forceinline__ int prep_row_hi(int y0, int H, int th, int tiles) {
-  const int y = y0 + kM3H < H - 1 ? y0 + kM3H : H - 1;
-  return y / th + 1 < tiles - 1 ? y / th + 1 : tiles - 1;
-}
-__host__ __device__ __forceinline__ int prep_row_lo(int y0, int th) {
-  const int y = y0 > 0 ? y0 - 1 : 0;
-  return y / th - 1 > 0 ? y / th - 1 : 0;
-}
-
-template <bool LB>
-__global__ __launch_bounds__(256) void prep_oneread_kernel(const uint8_t* __restrict__ in,
-                                                           uint8_t* __restrict__ out,
-                                                           uint8_t* __restrict__ lut, int H, int W,
-                                                           int pitch, int vec, ClaheGeo g, LbFuse lb,
-                                                           PrepQueue Q) {
-  __shared__ int s_next;
-  __shared__ unsigned long long s_seen;
-  const int tid = threadIdx.x;
-  const int home = xcc_id();
-  for (int qi = 0; qi < 8; ++qi) {
-    const int q = (home + qi) & 7;
-    const int nf = Q.B > q ? (Q.B - q + 7) >> 3 : 0;
-    const int total = nf * Q.per_frame;
-    if (total == 0) continue;
-    __syncthreads();
-    if (tid == 0) s_next = atomicAdd(&Q.ctr[q], 1);
-    __syncthreads();
-    // the item index comes through LDS: readfirstlane tells the compiler it
-    // is wave-uniform, so every derived address stays scalar (158 -> ~90 VGPRs)
-    int it = __builtin_amdgcn_readfirstlane(s_next);
-    unsigned long long known = 0;  // LUT rows of frame known_b seen complete
-    int known_b = -1;
-    while (it < total) {
-      const int fl = it / Q.per_frame;
-      const int b = q + 8 * fl;
-      int r = it - fl * Q.per_frame;
-      // a frame's items: the slices of LUT rows 0 .. ahead-1, then per k the
-      // slices of LUT row k + ahead and the blocks whose rows are all <= k
-      const int TS = Q.tiles * kPrepSlices;
-      bool is_lut = false;
-      int idx = 0, jb0 = 0, lrow = 0;
-      if (r < Q.ahead * TS) {
-        is_lut = true;
-        lrow = r / TS;
-        r -= lrow * TS;
-      } else {
-        r -= Q.ahead * TS;
-        for (int k = 0; k < Q.tiles; ++k) {
-          if (k + Q.ahead < Q.tiles) {
-            if (r < TS) {
-              is_lut = true;
-              lrow = k + Q.ahead;
-              break;
-            }
-            r -= TS;
-          }
-          const int nb = (Q.rows_end[k] - jb0) * Q.ntx;
-          if (r < nb) {
-            idx = jb0 * Q.ntx + r;
-            break;
-          }
-          r -= nb;
-          jb0 = Q.rows_end[k];
-        }
-      }
-      int slice = 0;
-      if (is_lut) {  // r: slice item within the row, tile-major
-        idx = lrow * Q.tiles + r / kPrepSlices;
-        slice = r - (r / kPrepSlices) * kPrepSlices;
-      }
-      int* rows = Q.ctr + kPrepCtr0 + b * Q.tiles;
-      if (!is_lut) {
-        const int y0 = (idx / Q.ntx) * kM3H;
-        const int lo = prep_row_lo(y0, g.th), hi = prep_row_hi(y0, H, g.th, Q.tiles);
-        const unsigned long long need = (hi == 63 ? ~0ull : (2ull << hi) - 1) & ~((1ull << lo) - 1);
-        if (known_b != b) {
-          known = 0;
-          known_b = b;
-        }
-        if ((known & need) != need) {
-          if (tid == 0) {
-            unsigned long long seen = 0;
-            for (int spin = 0;; ++spin) {
-              seen = 0;
-              for (int ty = lo; ty <= hi; ++ty)
-                if (__hip_atomic_load(rows + ty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= Q.tiles)
-                  seen |= 1ull << ty;
-              if ((seen & need) == need) break;
-              if (spin >= (1 << 22)) {  // never hang the box: flag it and go on
-                __hip_atomic_store(Q.ctr + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-              }
-              __builtin_amdgcn_s_sleep(2);
-            }
-            s_seen = seen;
-          }
-          __syncthreads();
-          known |= __builtin_amdgcn_readfirstlane((uint32_t)s_seen) |
-                   ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(s_seen >> 32)) << 32);
-        }
-      }
-      // claim the next item now: its latency overlaps this item's work
-      int nxt = 0;
-      if (tid == 0) nxt = atomicAdd(&Q.ctr[q], 1);
-      if (is_lut) {
-        const int hs = (g.th + kPrepSlices - 1) / kPrepSlices;
-        const int tt = b * Q.tiles * Q.tiles + idx;
-        LutSlice sl;
-        sl.r_lo = min(slice * hs, g.th);
-        sl.r_hi = min(sl.r_lo + hs, g.th);
-        sl.slice = slice;
-        sl.nslice = kPrepSlices;
-        sl.part = Q.part + (size_t)tt * kPrepSlices * 256;
-        sl.tile_ctr = Q.ctr + kPrepCtr0 + Q.B * Q.tiles + tt;
-        if (clahe_lut_body<kYCrCb, true>(in, lut, H, W, pitch, g, idx, b, opaque_tid(), &sl)) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();
-          if (tid == 0)
-            __hip_atomic_fetch_add(rows + idx / Q.tiles, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      } else {
-        const int by = idx / Q.ntx, bx = idx - by * Q.ntx;
-        med3_body<true, LB, true>(in, out, lut, H, W, pitch, vec, g, lb, b, bx * kM3W, by * kM3H,
-                                  opaque_tid());
-      }
-      __syncthreads();  // LDS of this item no longer read
-      if (tid == 0) s_next = nxt;
-      __syncthreads();
-      it = __builtin_amdgcn_readfirstlane(s_next);
-    }
-  }
-}
-
 static size_t lut_bytes(int B, int tiles) { return (size_t)B * tiles * tiles * 256; }
-static size_t prep_ctr_ints(int B, int tiles) { return kPrepCtr0 + (size_t)B * tiles * (1 + tiles); }
-static size_t prep_ctr_bytes(int B, int tiles) { return (prep_ctr_ints(B, tiles) * 4 + 255) & ~(size_t)255; }
-
-static bool prep_queue(const ClaheGeo& g, int H, int W, int B, uint8_t* ws, PrepQueue& Q) {
-  if (g.tiles > kPrepMaxTiles) return false;
-  Q.tiles = g.tiles;
-  Q.ntx = ceil_div(W, kM3W);
-  const int nty = ceil_div(H, kM3H);
-  Q.per_frame = g.tiles * g.tiles * kPrepSlices + Q.ntx * nty;
-  Q.B = B;
-  Q.ahead = std::min(kPrepAhead, g.tiles);
-  Q.ctr = (int*)(ws + lut_bytes(B, g.tiles));
-  Q.part = (int*)(ws + lut_bytes(B, g.tiles) + prep_ctr_bytes(B, g.tiles));
-  for (int k = 0; k < kPrepMaxTiles; ++k) {
-    int n = 0;
-    while (n < nty && prep_row_hi(n * kM3H, H, g.th, g.tiles) <= k) ++n;
-    Q.rows_end[k] = n;
-  }
-  return Q.rows_end[g.tiles - 1] == nty;
-}
-
-// RV_PREP_ONEREAD=1 selects the single-read pass (read per call).  Off by
-// default: it reads 287 MB per 32 x 1080p step instead of 410 MB (PMC), but
-// its LUT items (one workgroup per 240 x 135 tile, latency-bound at ~16 us)
-// starve the blocks queued behind them: bench 27.1 / 28.0k against 38.6k
-// frames/s (profiles/r03/prep_oneread_ab.txt).
-static bool prep_oneread_on() {
-  const char* e = getenv("RV_PREP_ONEREAD");
-  return e && atoi(e) != 0;
-}
 
 // Host checks for med3_kernel.
 // Upper bound of ncx * ncy in the kernel: distinct floor(p/t - 0.5) over a
@@ -1268,12 +1002,10 @@ static int check_frames(const uint8_t* in, const void* out, int B, int H, int W,
   return RV_OK;
 }
 
-// B x tiles^2 LUTs, then the single-read pass's counters and partial
-// histograms (RV_PREP_ONEREAD=1)
+// B x tiles^2 LUTs of 256 bytes
 extern "C" size_t rv_clahe_ws_bytes(int B, int tiles) {
   if (B <= 0 || tiles <= 0) return 0;
-  return lut_bytes(B, tiles) + prep_ctr_bytes(B, tiles) +
-         (size_t)B * tiles * tiles * kPrepSlices * 256 * 4;
+  return lut_bytes(B, tiles);
 }
 
 extern "C" int rv_clahe_ycrcb_u8(const uint8_t* in, uint8_t* out, int B, int H, int W, int pitch,
@@ -1418,29 +1150,6 @@ extern "C" int rv_clahe_median_letterbox_u8(const uint8_t* in, uint8_t* out, int
   uint8_t* lut = (uint8_t*)ws;
   st = launch_letterbox_pad(lb_out, B, lb.g, s);
   if (st) return st;
-  PrepQueue Q;
-  if (prep_oneread_on() && prep_queue(g, H, W, B, lut, Q)) {
-    const int vec = (pitch % 4 == 0) && (((uintptr_t)in) % 4 == 0) && (((uintptr_t)out) % 4 == 0);
-    const size_t cell_bytes = (size_t)med3_cells(g) * 1024;
-    static int occ = 0;
-    if (!occ) {
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, prep_oneread_kernel<true>, 256,
-                                                       cell_bytes) != hipSuccess || occ < 1)
-        occ = 1;
-      (void)hipGetLastError();
-    }
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipGetLastError();
-    hipError_t e = hipMemsetAsync(Q.ctr, 0, prep_ctr_ints(B, tiles) * 4, s);
-    if (e != hipSuccess) return launch_status("rv_clahe_median_letterbox_u8 (memset)");
-    const int items = B * Q.per_frame;
-    const char* wg = getenv("RV_PREP_WGS");  // A/B probe: workgroups of the persistent grid
-    const int grid = std::min(items, std::max(8, wg ? atoi(wg) : ncu * occ));
-    prep_oneread_kernel<true><<<grid, 256, cell_bytes, s>>>(in, out, lut, H, W, pitch, vec, g, lb, Q);
-    return launch_status("rv_clahe_median_letterbox_u8");
-  }
   launch_clahe_lut<kYCrCb>(in, lut, B, H, W, pitch, g, s);
   launch_med3<true, true>(in, out, lut, B, H, W, pitch, g, lb, s);
   return launch_status("rv_clahe_median_letterbox_u8");

@@ -20,6 +20,7 @@
 //
 // Host-array arguments (the letterbox geometry, SORT's parameter block and
 // homography) are copied into the node at record time.
+#include <atomic>
 #include <vector>
 #include <stdlib.h>
 #include <string.h>
@@ -49,6 +50,13 @@ struct Schedule {
   hipEvent_t fork = nullptr;
   std::vector<hipEvent_t> join;
   int64_t runs = 0;
+  // run generations: a run stamps every record node it issues with its
+  // generation; done_gen is the generation of the latest run that issued all
+  // its nodes (-1 while a run is issuing or after a failed one).  A host wait
+  // is valid only on an event of run done_gen.
+  std::vector<int64_t> ev_gen;
+  std::atomic<int64_t> gen{0};
+  std::atomic<int64_t> done_gen{-1};
 };
 
 template <class T>
@@ -197,6 +205,7 @@ extern "C" int rv_sched_add_record(void* handle, void* stream, int timing, int* 
                         : new_event(&e);
   if (st) return st;
   S->events.push_back(e);
+  S->ev_gen.push_back(-1);
   const int id = (int)S->events.size() - 1;
   Node n;
   n.kind = kRecord;
@@ -228,6 +237,10 @@ extern "C" int rv_sched_event_sync(void* handle, int event) {
   RV_CHECK_ARG(handle != nullptr, "null handle");
   Schedule* S = static_cast<Schedule*>(handle);
   RV_CHECK_ARG(event >= 0 && event < (int)S->events.size(), "rv_sched_event_sync: event %d", event);
+  const int64_t g = S->done_gen.load();
+  RV_CHECK_ARG(g >= 0 && S->ev_gen[event] == g,
+               "rv_sched_event_sync: event %d was not issued by the latest completed run (call it "
+               "after rv_sched_run returned without error)", event);
   // poll (default): query + short sleeps, so a waiting consumer never enters
   // the runtime's blocking wait while another thread is still issuing;
   // RV_SCHED_WAIT=sync: hipEventSynchronize
@@ -248,6 +261,9 @@ extern "C" int rv_sched_event_elapsed(void* handle, int a, int b, float* ms) {
   Schedule* S = static_cast<Schedule*>(handle);
   const int n = (int)S->events.size();
   RV_CHECK_ARG(a >= 0 && a < n && b >= 0 && b < n, "rv_sched_event_elapsed: events %d %d", a, b);
+  const int64_t g = S->done_gen.load();
+  RV_CHECK_ARG(g >= 0 && S->ev_gen[a] == g && S->ev_gen[b] == g,
+               "rv_sched_event_elapsed: events %d %d were not issued by the latest completed run", a, b);
   return hip_check(hipEventElapsedTime(ms, S->events[a], S->events[b]),
                    "rv_sched hipEventElapsedTime");
 }
@@ -266,6 +282,8 @@ extern "C" int rv_sched_run(void* handle, void* origin) {
     if (st) return st;
     S->join.push_back(e);
   }
+  S->done_gen.store(-1);
+  const int64_t gen = S->gen.fetch_add(1) + 1;
   int st = hip_check(hipEventRecord(S->fork, o), "rv_sched fork record");
   for (hipStream_t x : S->streams)
     if (!st && x != o) st = hip_check(hipStreamWaitEvent(x, S->fork, 0), "rv_sched fork wait");
@@ -275,6 +293,7 @@ extern "C" int rv_sched_run(void* handle, void* origin) {
       st = issue_op(n);
     } else if (n.kind == kRecord) {
       st = hip_check(hipEventRecord(S->events[n.event], n.st), "rv_sched hipEventRecord");
+      if (!st) S->ev_gen[n.event] = gen;
     } else {
       st = hip_check(hipStreamWaitEvent(n.st, S->events[n.event], 0), "rv_sched hipStreamWaitEvent");
     }
@@ -288,6 +307,9 @@ extern "C" int rv_sched_run(void* handle, void* origin) {
     if (!e) e = hip_check(hipStreamWaitEvent(o, S->join[k], 0), "rv_sched join wait");
     if (!st) st = e;
   }
-  if (!st) S->runs++;
+  if (!st) {
+    S->runs++;
+    S->done_gen.store(gen);
+  }
   return st;
 }

@@ -1297,6 +1297,43 @@ extern "C" int rv_yolo_profile_read(void* h, double* ms, double* flops, int* con
   return P.n_fwd;
 }
 
+// After the profiled forwards (synchronises): the [start, end) interval of
+// every recorded conv launch of handle h, in ms after the first recorded
+// event of handle `ref` (forward 0; ref may be h).  Handles of one device
+// share the clock, so the intervals of several forward contexts (lanes)
+// can be merged into the chip-wide busy time of the conv family.  Writes
+// at most n pairs; returns the number of intervals.
+extern "C" int rv_yolo_profile_times(void* h, void* ref, double* t0, double* t1, int n) {
+  RV_CHECK_ARG(h && ref && (n == 0 || (t0 && t1)), "bad args");
+  Model* M = (Model*)h;
+  const Profile& P = M->prof;
+  const Profile& R = ((Model*)ref)->prof;
+  if (!P.on || !R.on || R.n_fwd == 0) return 0;
+  hipEvent_t e0 = nullptr;
+  for (int i = 0; i < R.per_fwd && !e0; ++i)
+    if (R.conv_of[i] >= 0) e0 = R.ev[(size_t)i * 2];
+  if (!e0) return 0;
+  int k = 0;
+  for (int f = 0; f < P.n_fwd; ++f)
+    for (int i = 0; i < P.per_fwd; ++i) {
+      if (P.conv_of[i] < 0) continue;
+      hipEvent_t a = P.ev[((size_t)f * P.per_fwd + i) * 2], b = P.ev[((size_t)f * P.per_fwd + i) * 2 + 1];
+      float ta = 0.f, tb = 0.f;
+      if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ta, e0, a) != hipSuccess ||
+          hipEventElapsedTime(&tb, e0, b) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("rv_yolo_profile_times: event query failed");
+        return RV_EINVAL;
+      }
+      if (k < n) {
+        t0[k] = ta;
+        t1[k] = tb;
+      }
+      ++k;
+    }
+  return k;
+}
+
 // ---- per-layer autotuning ---------------------------------------------------
 namespace rv {
 

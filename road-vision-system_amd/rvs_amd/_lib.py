@@ -113,6 +113,7 @@ _SIGS = {
     "rv_yolo_profile_reps": (c_int, [c_void_p, c_int, c_int]),
     "rv_yolo_profile_read": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
     "rv_yolo_profile_bytes": (c_int, [c_void_p, c_void_p, c_int]),
+    "rv_yolo_profile_times": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
     "rv_yolo_autotune": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_int, c_int,
                                  POINTER(c_int), c_void_p]),
     "rv_yolo_tuned_config": (c_int, [c_void_p, c_int, POINTER(c_int)]),
@@ -165,6 +166,8 @@ def load():
     # never to a second copy from /opt/rocm: two runtimes in one process do not share devices
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
+        if not hasattr(lib, name) and _variant != "default":
+            continue  # an older A/B build (RV_LIB_VARIANT) without this entry
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -194,7 +197,7 @@ _RECORDABLE = {"rv_clahe_median_letterbox_u8", "rv_clahe_median_u8", "rv_letterb
 
 _NOCHECK = {"rv_sched_num_nodes", "rv_abi_version", "rv_cand_segments", "rv_yolo_cand_segments", "rv_clahe_median_fits", "rv_clahe_median_letterbox_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
             "rv_yolo_num_buffers", "rv_yolo_trace", "rv_yolo_profile_read", "rv_yolo_tuned_config",
-            "rv_yolo_profile_bytes", "rv_yolo_buffer_esize", "rv_yolo_conv_candidates"}
+            "rv_yolo_profile_bytes", "rv_yolo_profile_times", "rv_yolo_buffer_esize", "rv_yolo_conv_candidates"}
 
 
 _recorder = None  # a schedule.Schedule while one is being recorded
@@ -239,8 +242,15 @@ def stream_ptr(stream=None) -> int:
 
 
 def ptr(t) -> int:
-    """Device pointer of a torch tensor (None -> 0)."""
-    return 0 if t is None else int(t.data_ptr())
+    """Device pointer of a torch tensor (None -> 0).  While a schedule is
+    being recorded, the schedule keeps the tensor alive: a recorded node
+    holds the raw pointer, so a temporary made for the call (a .contiguous()
+    copy, a freshly grown workspace) must outlive every later run()."""
+    if t is None:
+        return 0
+    if _recorder is not None:
+        _recorder.keep(t)
+    return int(t.data_ptr())
 
 
 def int_array(vals):

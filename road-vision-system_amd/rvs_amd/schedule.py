@@ -85,6 +85,12 @@ class Schedule:
         h = ctypes.c_void_p()
         _lib.call("rv_sched_create", ctypes.byref(h))
         self.h = h
+        self._keep: Dict[int, torch.Tensor] = {}  # tensors whose pointers nodes hold
+
+    def keep(self, t) -> None:
+        """Hold `t` until close(): a node recorded its device pointer
+        (rvs_amd._lib.ptr calls this while recording)."""
+        self._keep[id(t)] = t
 
     def add(self, name: str, args) -> None:
         op, si, host = _OPS[name]
@@ -148,6 +154,7 @@ class Schedule:
         if self.h:
             _lib.load().rv_sched_destroy(self.h)
             self.h = None
+        self._keep = {}
 
     def __del__(self):
         try:

@@ -40,6 +40,18 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
+def gather_over_ranks(value: float, device=None) -> List[float]:
+    """Every rank's value of a per-rank scalar, in rank order ([value]
+    without a process group)."""
+    if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
+        return [float(value)]
+    n = torch.distributed.get_world_size()
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(n)]
+    torch.distributed.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
 def job_throughput(frames_per_rank: int, world: int, elapsed_max_s: float) -> float:
     """Whole-job frames/s: every rank's frames over the slowest rank's time."""
     return frames_per_rank * world / elapsed_max_s
@@ -71,7 +83,8 @@ def timed_job(run: Callable[[], None], sync: Callable[[], None], units_per_rank:
     """The timed region every rank runs: barrier + device sync, `run()` (the
     K steps), device sync, barrier; the elapsed time is reduced with a MAX
     over ranks and the whole-job rate is all ranks' units over that time.
-    Returns {"local_s", "elapsed_s" (max over ranks), "value"}."""
+    Returns {"local_s", "per_rank_s" (every rank's local_s, rank order),
+    "elapsed_s" (max over ranks), "value"}."""
     world = torch.distributed.get_world_size() if (
         torch.distributed.is_available() and torch.distributed.is_initialized()) else 1
     _barrier()
@@ -82,5 +95,6 @@ def timed_job(run: Callable[[], None], sync: Callable[[], None], units_per_rank:
     local = time.perf_counter() - t0
     _barrier()
     elapsed = max_over_ranks(local, device)
-    return {"local_s": local, "elapsed_s": elapsed,
+    per_rank = gather_over_ranks(local, device)
+    return {"local_s": local, "per_rank_s": per_rank, "elapsed_s": elapsed,
             "value": job_throughput(units_per_rank, world, elapsed)}

@@ -2,7 +2,7 @@
 stem_kernel): the packer's balanced base-256 i8 digits reconstruct integers
 Q = round(V / s) of V = w[rgb][ky][kx] / 255 at 2^-23 of each channel's
 largest |V|; the kernel's per-digit sums (accumulators started at
-128 sum D_i) are exact and below 2^24; and s (65536 T0 + 256 T1 + T2) + b,
+128 sum D_i) are exact and below 2^24; and s (65536 T0 + (256 T1 + T2)) + b,
 evaluated in f32 in the kernel's order, equals the f64 conv of x / 255 (BGR
 window bytes, the reference's RGB order) to ~2^-22 of the output scale --
 far inside the 1 bf16 ulp (+1e-6) the GPU layer test allows."""
@@ -55,7 +55,9 @@ def test_conv0_digits_and_value():
             np.testing.assert_array_equal(acc, x @ d[i].T)
             assert np.abs(acc).max() < 2 ** 24
             T.append(acc.astype(np.float32))
-        u = (T[0] * np.float32(65536) + T[1] * np.float32(256)).astype(np.float32) + T[2]
+        # the kernel's combine: 256 T1 + T2 exactly in i32, then one fma
+        t12 = (T[1].astype(np.int64) * 256 + T[2].astype(np.int64)).astype(np.float32)
+        u = (T[0].astype(np.float64) * 65536 + t12.astype(np.float64)).astype(np.float32)
         got = (s[None, :] * u + b[None, :]).astype(np.float64)
         ref = x @ V.T + b.astype(np.float64)
         scale = np.abs(V).sum(1) * 255 + np.abs(b)

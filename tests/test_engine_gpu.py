@@ -198,6 +198,46 @@ def test_native_schedule_replays(cuda):
     assert ids0 and ids1
 
 
+def test_native_schedule_keeps_temporaries_and_checks_runs(cuda):
+    """A recorded node holds raw device pointers: the schedule must keep the
+    temporaries made while recording alive (here the .contiguous() copies of
+    stream-interleaved frame views), so runs after the memory was churned
+    still read the right frames.  rv_sched_event_sync refuses an event
+    before the first run (no stale or unwritten record is ever handed out)."""
+    from rvs_amd._lib import RVError
+    from rvs_amd.engine import RoadVisionEngine
+    from rvs_amd.schedule import PipelinedRun
+    from rvs_amd.synth import road_frames
+    cfg = _cfg()
+    S, H, W, K = 2, 720, 1280, 2
+    frames = road_frames(S, K, H, W, device=cuda)
+    ts = [torch.full((S,), k / 30.0, dtype=torch.float64, device=cuda) for k in range(K)]
+    # (H, S, W, 3) storage viewed as (S, H, W, 3): not the ABI's pitch layout
+    views = []
+    for k in range(K):
+        inter = torch.empty((H, S, W, 3), dtype=torch.uint8, device=cuda)
+        inter.copy_(frames[k].permute(1, 0, 2, 3))
+        views.append(inter.permute(1, 0, 2, 3))
+    assert not views[0].is_contiguous()
+    eng = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=2, pair=2)
+    run = PipelinedRun(eng, views, ts, mode="native")
+    with pytest.raises(RVError):
+        run.wait_step(0)  # no run yet
+    torch.cuda.synchronize()
+    churn = [torch.full((S, H, W, 3), 7, dtype=torch.uint8, device=cuda) for _ in range(4)]
+    run.run()
+    run.wait_step(K - 1)
+    torch.cuda.synchronize()
+    for k, o in enumerate(run.outs):
+        src = frames[k].cpu().numpy()
+        pr = o["proc"].cpu().numpy()
+        for s in range(S):
+            np.testing.assert_array_equal(pr[s], cpu.median(cpu.clahe_ycrcb(src[s]), 3))
+    del churn
+    run.close()
+    eng.close()
+
+
 @pytest.mark.parametrize("pair", [1, 4])
 def test_bench_configuration_parity(cuda, pair):
     """Exactly bench.py's timed configuration (S = 32 streams of 1080p,

@@ -255,8 +255,9 @@ def test_fp8_network_matches_fp8_oracle(cuda, H, W, variant):
     (fp8 rounding lowers scores: fp32 has ~1.5x the detections; measured
     on the CPU oracles 95 %).  YOLOv8n keeps the plain He-normal weights its
     bf16 bench and tests use; those are chaotic in fp8 (the oracle keeps 21 %
-    of its detections under the same perturbation), so only loose bars
-    apply there."""
+    of its detections under the same perturbation), so YOLOv8n fp8 is NOT a
+    parity target: its loose bars (40 % at IoU 0.5, score p99.9 <= 0.15)
+    only check that the plan runs and stays in the oracle's neighbourhood."""
     B, keep = 2, [0, 2, 3, 5, 7]
     eng, flat = _engine(variant, H, W, B, cuda, seed=0, classes_keep=keep)
     fr = np.stack([cpu.median(cpu.clahe_ycrcb(road_frame(H, W, seed=20 + b)), 3)
@@ -328,7 +329,12 @@ def test_fp8_config5_fog_1280(cuda):
     print(f"config5 fp8 vs bf16 plan (IoU 0.5): {h1}/{t1} bf16 dets matched, {h2}/{t2} fp8 "
           f"dets matched; IoU 0.9: {_match(got16, got8)}, {_match(got8, got16)}")
     # fp8 rounding lowers scores (the bf16 plan keeps more detections): most
-    # fp8 detections must be bf16 ones
-    assert t1 > 0 and t2 > 0 and h2 >= 0.8 * t2
+    # fp8 detections must be bf16 ones (precision), and at least half of the
+    # bf16 plan's detections must survive in fp8 (recall; fp32 keeps ~1.5x
+    # the fp8 detections, so the floor sits below 1 / 1.5).  The YOLOv8m
+    # fixture weights carry a channel-coherent share chosen for fp8
+    # conditioning (weights.base_weights): no real checkpoint
+    # pins this parity figure.
+    assert t1 > 0 and t2 > 0 and h2 >= 0.8 * t2 and h1 >= 0.5 * t1
     eng.close()
     e16.close()

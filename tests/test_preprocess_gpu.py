@@ -169,42 +169,6 @@ def test_fused_letterbox_equals_chain(cuda, H, W):
     np.testing.assert_array_equal(lb[0].cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("B", [11, 32])
-def test_single_read_pass_repeated(cuda, B, monkeypatch):
-    """rv_clahe_median_letterbox_u8 runs as one persistent launch whose
-    workgroups hand the tile LUTs to each other (per-XCD queues, sc1 stores
-    and loads, agent-scope row counters).  Ragged (11 frames: queues of 2
-    and 1 frames) and full (32) batches, 8 launches each with a different
-    frame order and a side stream loading the GPU: every launch's proc and
-    letterbox must equal the two-launch chain byte for byte."""
-    import torch
-    from rvs_amd import kernels
-    monkeypatch.setenv("RV_PREP_ONEREAD", "1")  # opt-in path (read per call)
-    H, W = 1080, 1920
-    frames = np.stack([road_frame(H, W, seed=300 + b) for b in range(B)])
-    geo = kernels.letterbox_geometry(H, W)
-    x = _dev(frames, cuda)
-    chain = kernels.clahe_median(x, 8, 2.0, 3).cpu().numpy()  # always two launches
-    lb_ref = kernels.letterbox(torch.from_numpy(chain).to(cuda), geo).cpu().numpy()
-    side = torch.cuda.Stream(device=cuda)
-    big = torch.randn(4096, 4096, device=cuda)
-    rng = np.random.default_rng(7)
-    ws = torch.empty(kernels.clahe_ws_bytes(B, 8), dtype=torch.uint8, device=cuda)
-    # the pass's timeout flag: int 8 of the counters after the B x 64 LUTs
-    flag = ws[B * 64 * 256 + 32:B * 64 * 256 + 36]
-    for rep in range(8):
-        perm = rng.permutation(B)
-        xp = x[torch.from_numpy(perm).to(cuda)].contiguous()
-        with torch.cuda.stream(side):  # uneven load beside the pass
-            for _ in range(4):
-                big = big @ big * 1e-3
-        proc, lb = kernels.clahe_median_letterbox(xp, 8, 2.0, 3, geo, ws=ws)
-        np.testing.assert_array_equal(proc.cpu().numpy(), chain[perm], err_msg=f"rep {rep}")
-        np.testing.assert_array_equal(lb.cpu().numpy(), lb_ref[perm], err_msg=f"rep {rep}")
-        assert not flag.cpu().numpy().any(), f"rep {rep}: a LUT wait timed out"
-    torch.cuda.synchronize(cuda)
-
-
 @pytest.mark.parametrize("H,W,tiles,clip", [(1080, 1920, 8, 2.0), (640, 640, 8, 2.0),
                                             (37, 91, 3, 2.0), (480, 640, 8, 0.0),
                                             (721, 1283, 5, 4.0)])

@@ -115,6 +115,7 @@ def test_two_rank_sharding_matches_single_process():
     mx = max(r[3]["local_s"] for r in res)
     assert all(r[3]["local_s"] > 0 for r in res)
     assert all(r[3]["elapsed_s"] == mx for r in res)
+    assert all(r[3]["per_rank_s"] == [x[3]["local_s"] for x in res] for r in res)
     assert all(abs(r[3]["value"] - S * F * world / mx) < 1e-9 * r[3]["value"] for r in res)
     # each rank's per-stream results equal a single process running all streams
     import sys
@@ -158,14 +159,21 @@ def test_bench_gpus_flag_spawns_the_ranks(tmp_path, capfd, monkeypatch):
     monkeypatch.setenv("OMP_NUM_THREADS", "2")
     S, F = 2, 3
     rc = bench.main(["--gpus", "2", "--streams", str(S), "--steps", str(F), "--warmup", "0",
+                     "--cpu-frames", "1", "--cpu-workers", "1",
                      "--job", "test_shard_gloo:_CpuJob"])
     assert rc == 0
     lines = [ln for ln in capfd.readouterr().out.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["steps"] == F
-    assert abs(d["value"] - S * F * 2 / d["elapsed_s"]) < 1e-9 * d["value"]
+    assert abs(d["value"] - S * F * 2 / d["elapsed_s"]) < 1e-4 * d["value"]  # elapsed_s rounded to 1 us
     assert d["elapsed_s"] >= d["local_s"] > 0
+    # every rank's own timed-region time, and the reported time is their max
+    assert len(d["per_rank_local_s"]) == 2 and all(x > 0 for x in d["per_rank_local_s"])
+    assert abs(max(d["per_rank_local_s"]) - d["elapsed_s"]) < 1e-5
+    # the CPU baseline rides in the N > 1 line too (rank 0, after the barrier)
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 0
     merged = {}
     for r in range(2):
         merged.update({int(k): [(a, b) for a, b in v] for k, v in

@@ -3,14 +3,18 @@ trace: keeps the dispatches between the two rv_trace_marker kernels bench.py
 launches right before and right after its timed region (tags 1 and 2), so
 warm-up, autotuning, capture and the CPU baseline are excluded.
 
-usage: python tools/trace_window.py kernel_trace.csv STEPS OUT_PREFIX [PAIR]
-PAIR (default 0) picks the window between marker dispatches 2*PAIR and
-2*PAIR+1: 0 = the timed region, 1 = bench.py's in-pipeline conv profiling
-pass, 2 = its eager conv profiling pass (--conv-timing both).
+usage: python tools/trace_window.py kernel_trace.csv STEPS OUT_PREFIX [A,B]
+A,B (default 1,2) are the marker tags bracketing the window: the first
+marker of tag A and the first marker of tag B after it.  rv_trace_marker
+launches `tag` workgroups of 64, so a dispatch's tag is Grid_Size_X / 64.
+bench.py's tags: 1,2 the timed region; 3,4 the in-pipeline conv profiling
+pass; 5,6 the eager conv profiling pass (5 repetitions of every launch);
+7,8 the device-only rerun of the timed region.
 writes OUT_PREFIX_kernel_stats.csv (rocprofv3 --stats columns) and
 OUT_PREFIX_summary.txt (per-step time of each kernel family, conv family
 included, and the window's wall time)."""
 import csv
+import gzip
 import sys
 from collections import defaultdict
 
@@ -22,21 +26,31 @@ def family(name: str) -> str:
     return base.split("<")[0].split("::")[-1]
 
 
+def marker_window(rows, ta, tb):
+    """Row indices of the first marker of tag ta and the first marker of tag
+    tb after it (rows: (start, end, name, tag) sorted by start)."""
+    marks = [(i, r[3]) for i, r in enumerate(rows) if "rv_trace_marker_kernel" in r[2]]
+    a = next((i for i, t in marks if t == ta), None)
+    b = next((i for i, t in marks if t == tb and a is not None and i > a), None)
+    if a is None or b is None:
+        sys.exit(f"no marker window {ta} -> {tb}: markers {[t for _, t in marks]}")
+    return a, b
+
+
 def main():
     path, steps, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
-    pair = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    tags = [int(x) for x in (sys.argv[4] if len(sys.argv) > 4 else "1,2").split(",")]
     rows = []
-    for r in csv.DictReader(open(path)):
-        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    opener = gzip.open(path, "rt") if path.endswith(".gz") else open(path)
+    for r in csv.DictReader(opener):
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
+                     int(r.get("Grid_Size_X") or 64) // 64))
     rows.sort()
-    marks = [i for i, r in enumerate(rows) if "rv_trace_marker_kernel" in r[2]]
-    if len(marks) < 2 * pair + 2:
-        sys.exit(f"need {2 * pair + 2} rv_trace_marker dispatches, found {len(marks)}")
-    a, b = marks[2 * pair], marks[2 * pair + 1]
+    a, b = marker_window(rows, tags[0], tags[1])
     win = rows[a + 1:b]
     t0, t1 = rows[a][1], rows[b][0]
     agg = defaultdict(list)
-    for s, e, n in win:
+    for s, e, n, _ in win:
         agg[n].append(e - s)
     tot = sum(sum(v) for v in agg.values())
     with open(out + "_kernel_stats.csv", "w", newline="") as f:
