@@ -51,7 +51,7 @@ PEAK_HBM = 8000.0                      # GB/s
 IMAGE_POINTS = [[560, 1000], [1360, 1000], [1160, 620], [760, 620]]
 WORLD_POINTS = [[-3.5, 5.0], [3.5, 5.0], [3.5, 30.0], [-3.5, 30.0]]
 METRIC = "end-to-end frames/sec @1080p (preproc+YOLOv8n+SORT), 1/2/4/8 MI355X"
-PMC_TRAFFIC = os.path.join(REPO, "profiles", "r03", "pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "r04", "pmc_traffic.json")
 LIB = os.path.join(REPO, "road-vision-system_amd", "rvs_amd", "librvhip.so")
 
 
@@ -205,6 +205,7 @@ class BenchJob:
         self.device_end = 0.0
         self.issue_s = 0.0
         self.tags = (1, 2)       # rv_trace_marker tags around the timed region
+        self.t_device_only = None  # local time of the device-only rerun
         self.sort_saved = None   # SORT state the timed region starts from
         torch.cuda.synchronize()
 
@@ -395,11 +396,12 @@ def _conv_pass(job, mode: str, tags):
     fl, by, cv = np.zeros(n), np.zeros(n), np.zeros(n, np.int32)
     t0s, t1s = [], []
     for h in hs:
-        ms = np.zeros(n)
-        nf = lib.rv_yolo_profile_read(h, ms.ctypes.data, fl.ctypes.data, cv.ctypes.data, n)
-        if nf <= 0:
+        ms, f1, c1, b1 = np.zeros(n), np.zeros(n), np.zeros(n, np.int32), np.zeros(n)
+        nf = lib.rv_yolo_profile_read(h, ms.ctypes.data, f1.ctypes.data, c1.ctypes.data, n)
+        if nf <= 0:  # a lane that ran no forward in this pass
             continue
-        lib.rv_yolo_profile_bytes(h, by.ctypes.data, n)
+        lib.rv_yolo_profile_bytes(h, b1.ctypes.data, n)
+        fl, cv, by = f1, c1, b1  # the same plan on every lane
         ms_tot += ms
         nf_tot += nf
         cnt = lib.rv_yolo_profile_times(h, hs[0], None, None, 0) \
@@ -438,19 +440,19 @@ def _lib_sha256() -> str:
 
 def pmc_traffic() -> dict:
     """HBM bytes per step of the conv family from rocprofv3 PMC passes
-    (tools/gpu_pmc.sh -> profiles/r03/pmc_traffic.json), reported only when
+    (tools/gpu_pmc.sh -> profiles/r04/pmc_traffic.json), reported only when
     they were collected on the library this run loaded (same sha256)."""
     if not os.path.exists(PMC_TRAFFIC):
         return {"traffic": None, "traffic_note": "no PMC pass of this round's library"}
     d = json.load(open(PMC_TRAFFIC))
     if d.get("librvhip_sha256") != _lib_sha256():
         return {"traffic": None,
-                "traffic_note": "the PMC passes in profiles/r03/pmc_traffic.json were collected "
+                "traffic_note": "the PMC passes in profiles/r04/pmc_traffic.json were collected "
                                 "on another build of librvhip.so: not reported"}
     return {"traffic": d.get("conv_bytes_per_step"),
             "traffic_unit": "HBM bytes per step, all conv launches (rocprofv3 PMC: 2 x "
                             "FETCH_SIZE + WRITE_SIZE, separate passes, this build; "
-                            "profiles/r03/pmc_traffic.json)"}
+                            "profiles/r04/pmc_traffic.json)"}
 
 
 def conv_roofline(job, mode: str) -> dict:
@@ -607,21 +609,41 @@ def cpu_baseline(cfg: dict, nfr: int, workers: int) -> dict:
                       f"each); slowest worker {slowest:.1f} s"}
 
 
-def steady_state(job) -> dict:
-    """The steady-state rate of the last (device-only) run: host times at
-    which the watcher saw each step handed back, from the last step of the
-    second pipeline unit (the pipeline is full) to the last step -- beside
-    the fill-and-drain rate of the timed region."""
-    done = job.cons.get("done")
-    P = job.eng.pair
-    k0 = 2 * P - 1
-    if not done or len(done) - 1 <= k0:
+def steady_state(job, mult: int = 3) -> dict:
+    """The pipeline's steady-state rate, free of its fill and drain: the same
+    schedule recorded over mult x K steps (the K timed frames cycled, fresh
+    timestamps), timed device-only like the rerun; the marginal rate of the
+    extra (mult - 1) K steps, (mult - 1) K S / (t(mult K) - t(K)), is the rate
+    of a pipeline that never fills or drains.  (r03 took hand-back
+    completion times inside one K-step run, which units of 4 steps complete
+    in bursts -- not a rate.)"""
+    from rvs_amd.schedule import PipelinedRun
+    from rvs_amd.shard import timed_job
+    if job.runner is None or job.unit_sizes is None:
         return {}
-    per = (done[-1] - done[k0]) / (len(done) - 1 - k0)
+    K, S, Wm = job.K, job.S, job.Wm
+    n = mult * K
+    ts = [torch.full((S,), (Wm + k) / 30.0, dtype=torch.float64, device=job.dev) for k in range(n)]
+    units = job.unit_sizes * mult
+    long_run = PipelinedRun(job.eng, [job.frames[Wm + (k % K)] for k in range(n)], ts,
+                            mode=job.args.exec_mode, sync=job.args.sync, units=units)
+    saved = job.eng.tracker.state[0].clone()
+    long_run.run()  # warm
+    torch.cuda.synchronize()
+    job.eng.tracker.state[0].copy_(saved)
+    t = timed_job(long_run.run, torch.cuda.synchronize, n * S, job.dev)
+    job.eng.tracker.state[0].copy_(saved)
+    long_run.close()
+    t1 = job.t_device_only
+    if t1 is None or t["local_s"] <= t1:
+        return {}
+    per = (t["local_s"] - t1) / ((mult - 1) * K)
     return {"steady_state_ms_per_step": round(per * 1e3, 4),
-            "steady_state_frames_per_s": round(job.S / per, 1),
-            "steady_state_window": f"hand-back completions of steps {k0}..{len(done) - 1} of the "
-                                   "device-only run (host clock, watcher thread)"}
+            "steady_state_frames_per_s": round(S / per, 1),
+            "steady_state_window": f"marginal rate of a {n}-step run of the same schedule (the K "
+                                   f"timed frames cycled) over the {K}-step device-only run: "
+                                   f"({n} - {K}) steps / (t({n}) - t({K}))",
+            f"device_only_{n}_steps_frames_per_s": round(n * S / t["local_s"], 1)}
 
 
 def _cpu_baseline_leg(args, rank: int, world: int, cfg) -> dict:
@@ -728,7 +750,8 @@ def main(argv=None):
     # the same K steps again without the consumer, from the same SORT state:
     # the device-only rate, and the steady state from its per-step completions
     t2 = rank_job_again(job, dev) if job.consume == "consume" else None
-    steady = steady_state(job)
+    job.t_device_only = t2["local_s"] if t2 is not None else None
+    steady = steady_state(job) if world == 1 else {}
     roof = conv_roofline(job, args.conv_timing) if args.conv_timing != "none" else None
     P = job.eng.pair
     execution = ("sequential step() calls (no pipelining)" if args.exec_mode == "sequential" else

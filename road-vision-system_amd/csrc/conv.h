@@ -65,7 +65,8 @@ struct ConvArgs {
 // weights, persistent grid.
 struct ConvCfg {
   int mr, nr, G, resw, persist;
-  int kind = 0;  // 0: LDS-staged patch kernel; 1: 1x1 direct-B kernel (G, resw unused)
+  int kind = 0;  // 0: LDS-staged patch kernel (4 waves); 1: 1x1 direct-B kernel (G, resw
+                 // unused); 2: the patch kernel with 8 waves per workgroup (bf16 3x3)
 };
 
 // Implicit-GEMM conv on MFMA (v_mfma_f32_16x16x32_bf16), default config.

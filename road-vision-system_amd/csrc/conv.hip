@@ -609,8 +609,12 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& a, f32x4 (&acc)[MR][NR
 // kernel's 32-channel chunk); each tap runs two v_mfma_f32_16x16x32_fp8_fp8
 // per chunk (channels 0-31 and 32-63), each lane reading 8 of its 16-B
 // quarter pair (logical quarter 2h + quad/2, byte (quad & 1) * 8).
-template <int MR, int NR, int K, int S, bool RESW, bool F8>
-__global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo g) {
+// NW = 8 (kind 2): one 512-thread workgroup per CU instead of two of 256,
+// so a resident weight slab (or a staged chunk of weights) is shared by 8
+// waves and the pixel tile is twice as large -- half the LDS-DMA bytes per
+// MFMA of the 4-wave form at the same occupancy (2 waves per SIMD).
+template <int MR, int NR, int K, int S, bool RESW, bool F8, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(ConvArgs a, PatchGeo g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int T2 = K * K;
   constexpr int BC = 16 * MR;
@@ -618,7 +622,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
   constexpr int MAXP = patch_maxit<NR, S>();
   static_assert(MAXP <= 32, "tail mask is 32 bits");
   constexpr int WJ = BC * T2 / 16;            // weight DMA instructions per chunk
-  constexpr int MAXW = (WJ + 3) / 4;
+  constexpr int MAXW = (WJ + NW - 1) / NW;
   constexpr int EB = F8 ? 1 : 2;              // bytes per element
   constexpr int CC = F8 ? 64 : 32;            // channels per chunk (64 B per pixel)
   const int tid = threadIdx.x;
@@ -719,7 +723,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
   int lgeo[MAXP];
 #pragma unroll
   for (int it = 0; it < MAXP; ++it) {
-    const int L = 64 * (wave + 4 * it) + lane;
+    const int L = 64 * (wave + NW * it) + lane;
     const int pix = L / SL, q = L - SL * pix;
     const int py = (int)(((float)pix + 0.5f) * inv_pw);
     const int sc = pix - py * g.PW;  // stored column
@@ -759,7 +763,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
   uint32_t wvoff[MAXW];
 #pragma unroll
   for (int it = 0; it < MAXW; ++it) {
-    const int j = wave + 4 * it;
+    const int j = wave + NW * it;
     const int pr = j * 16 + (lane >> 2);
     const int row = pr / T2, tap = pr - (pr / T2) * T2;
     const int q = (lane & 3) ^ swzq<F8>(row);
@@ -768,7 +772,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
   auto dma_weights = [&](int c, uint8_t* Wl) {
 #pragma unroll
     for (int it = 0; it < MAXW; ++it) {
-      const int j = wave + 4 * it;
+      const int j = wave + NW * it;
       if (j < WJ) dma16(w_rsrc, Wl + j * 1024, wvoff[it], c * 64);
     }
   };
@@ -780,7 +784,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(ConvArgs a, PatchGeo
       const bool tail = has_tail && c == nch - 1;
 #pragma unroll
       for (int it = 0; it < MAXP; ++it) {
-        const int j = wave + 4 * it;
+        const int j = wave + NW * it;
         if (j < g.pinst) {
           const uint32_t v = tail && ((tailbad >> it) & 1) ? kOOB : voff[it];
           dma16(img_rsrc, P + j * 1024, v, c * 64);
@@ -1085,13 +1089,14 @@ static int conv_nch(const ConvArgs& a) {
 static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& smem) {
   if (!((a.k == 1 || a.k == 3) && (a.stride == 1 || a.stride == 2) && a.pad == a.k / 2)) return false;
   const int NR = c.nr, MR = c.mr;
-  const int P = 64 * NR;
+  const int NW = c.kind == 2 ? 8 : 4;  // waves per workgroup
+  const int P = 16 * NR * NW;
   // tile width: the fewest halo-patch pixels DMA'd over the whole layer
   // (tiles x PH x PW, edge tiles included); at least 16 columns, so a B
   // fragment's 16 pixels mostly share one patch row (conflict-free reads)
   int C = 0;
   long best = -1;
-  for (int c = std::min(std::min(a.Wo, P), 64 * NR); c >= std::min(16, a.Wo); --c) {
+  for (int c = std::min(a.Wo, P); c >= std::min(16, a.Wo); --c) {
     const int r = P / c;
     const long cost = (long)ceil_div(a.Wo, c) * ceil_div(a.Ho, r) * ((r - 1) * a.stride + a.k) *
                       ((c - 1) * a.stride + a.k);
@@ -1114,7 +1119,7 @@ static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& 
   g.fast = epi_fast(a) ? 1 : 0;
   // per-lane offset registers of the kernel (patch_maxit)
   const int maxit = (a.stride == 2 ? 6 : 2) * NR + 2;
-  if (ceil_div(g.pinst, 4) > maxit) return false;
+  if (ceil_div(g.pinst, NW) > maxit) return false;
   const size_t wb = (size_t)16 * MR * a.k * a.k * 64;
   // two stages: the next (tile, chunk group) streams in during the current one
   smem = (c.resw ? nch * wb : 0) + 2 * (size_t)g.G * (g.p_bytes + (c.resw ? 0 : wb));
@@ -1137,11 +1142,11 @@ static int num_cus() {
 
 // Every instantiation gets the full 160 KB dynamic-LDS cap once; resident
 // blocks per CU are cached per LDS size (per instantiation).
-template <int MR, int NR, int K, int S, bool RESW, bool F8 = false>
+template <int MR, int NR, int K, int S, bool RESW, bool F8 = false, int NW = 4>
 static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, int persist,
                           hipStream_t s) {
   static bool attr = false;
-  auto fn = conv_patch_kernel<MR, NR, K, S, RESW, F8>;
+  auto fn = conv_patch_kernel<MR, NR, K, S, RESW, F8, NW>;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        160 * 1024);
@@ -1158,7 +1163,7 @@ static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, int
   for (int i = 0; i < 16; ++i)
     if (occ_smem[i] == smem) occ = occ_val[i];
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, smem) != hipSuccess || occ < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 64 * NW, smem) != hipSuccess || occ < 1)
       occ = 1;
     (void)hipGetLastError();
     for (int i = 0; i < 16; ++i)
@@ -1173,7 +1178,7 @@ static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, int
   const int ntiles = a.B * g.tiles_x * g.tiles_y;
   const int gx = xcd_grid(std::max(1, num_cus() * occ / ytiles), ntiles, persist != 0);
   dim3 grid(gx, ytiles);
-  fn<<<grid, 256, smem, s>>>(a, g);
+  fn<<<grid, 64 * NW, smem, s>>>(a, g);
   return launch_status("conv_patch");
 }
 
@@ -1285,13 +1290,39 @@ static int launch_patch_ks(const ConvArgs& a, const PatchGeo& g, size_t smem, in
   return RV_EINVAL;
 }
 
+// 8-wave patch kernel (kind 2): bf16 3x3 layers; 2 waves per SIMD leave
+// 256 VGPRs per lane, so no tile is excluded for register pressure
+template <int MR, int NR>
+constexpr bool tile_w8_built() {
+  return (MR == 8 && NR <= 2) || (MR == 5 && NR <= 2) || (MR == 4 && NR <= 4 && NR != 3) ||
+         (MR == 2 && NR == 4);
+}
+template <int MR, int NR, bool RESW>
+static int launch_patch8_ks(const ConvArgs& a, const PatchGeo& g, size_t smem, int persist,
+                            hipStream_t s) {
+  if constexpr (tile_w8_built<MR, NR>()) {
+    if (!a.in8 && a.k == 3 && a.stride == 1)
+      return launch_patch_t<MR, NR, 3, 1, RESW, false, 8>(a, g, smem, persist, s);
+    if constexpr (patch_s2_ok<MR, NR>())
+      if (!a.in8 && a.k == 3 && a.stride == 2)
+        return launch_patch_t<MR, NR, 3, 2, RESW, false, 8>(a, g, smem, persist, s);
+  }
+  set_error("conv_patch (8 waves): no variant MR=%d NR=%d k=%d s=%d", MR, NR, a.k, a.stride);
+  return RV_EINVAL;
+}
+static bool w8_tile(int mr, int nr) {
+  return (mr == 8 && nr <= 2) || (mr == 5 && nr <= 2) || (mr == 4 && (nr == 1 || nr == 2 || nr == 4)) ||
+         (mr == 2 && nr == 4);
+}
+
 // (MR, NR) tiles built for the patch kernel
 static const int kTiles[][2] = {{8, 2}, {8, 1}, {5, 2}, {5, 1}, {4, 4}, {4, 2}, {4, 1},
                                 {2, 4}, {2, 2}, {2, 1}, {1, 4}, {1, 2}, {1, 1}};
 
 bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c) {
   if (c.kind == 1) return !a.in8 && direct_ok(a, c);
-  if (c.kind != 0 || vcat(a)) return false;
+  if ((c.kind != 0 && c.kind != 2) || vcat(a)) return false;
+  if (c.kind == 2 && (a.in8 || a.k != 3 || !w8_tile(c.mr, c.nr))) return false;
   if (a.in8 && !((c.mr == 1 || c.mr == 2 || c.mr == 4) && (c.nr == 1 || c.nr == 2 || c.nr == 4)))
     return false;
   if (a.in8 && (a.Cin % 16 || a.in_co % 16 || a.in_cs % 16 ||
@@ -1301,7 +1332,7 @@ bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c) {
   if (c.mr > T && c.mr > 1) return false;
   if (a.stride == 2 && (c.nr > 2 || c.mr * c.nr > 8 || a.k != 3)) return false;  // patch_s2_ok
   if (a.g2_cout0 > 0 && a.g2_cout0 % (16 * c.mr) != 0) return false;  // tiles inside one group
-  if (patch_spills(c.mr, c.nr, a.k, a.stride, c.resw != 0)) return false;
+  if (c.kind == 0 && patch_spills(c.mr, c.nr, a.k, a.stride, c.resw != 0)) return false;
   if (a.in8 && patch_spills8(c.mr, c.nr, a.k, a.stride, c.resw != 0)) return false;
   PatchGeo g;
   size_t sm;
@@ -1311,7 +1342,7 @@ bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c) {
 int launch_conv_cfg(const ConvArgs& a, const ConvCfg& c, hipStream_t s) {
   PatchGeo g;
   size_t sm;
-  if (!conv_cfg_ok(a, c) || (c.kind == 0 && !patch_geo(a, c, g, sm))) {
+  if (!conv_cfg_ok(a, c) || (c.kind != 1 && !patch_geo(a, c, g, sm))) {
     set_error("conv config MR=%d NR=%d G=%d resw=%d not valid for this layer", c.mr, c.nr, c.G,
               c.resw);
     return RV_EINVAL;
@@ -1319,6 +1350,8 @@ int launch_conv_cfg(const ConvArgs& a, const ConvCfg& c, hipStream_t s) {
 #define RV_PATCH(M_, N_)                                                                     \
   if (c.mr == M_ && c.nr == N_)                                                              \
     return c.kind == 1 ? launch_direct_t<M_, N_>(a, c.persist, s)                            \
+           : c.kind == 2 ? (c.resw ? launch_patch8_ks<M_, N_, true>(a, g, sm, c.persist, s)    \
+                                   : launch_patch8_ks<M_, N_, false>(a, g, sm, c.persist, s))  \
            : c.resw    ? launch_patch_ks<M_, N_, true>(a, g, sm, c.persist, s)               \
                        : launch_patch_ks<M_, N_, false>(a, g, sm, c.persist, s);
   RV_PATCH(8, 2) RV_PATCH(8, 1) RV_PATCH(5, 2) RV_PATCH(5, 1) RV_PATCH(4, 4) RV_PATCH(4, 2)
@@ -1337,21 +1370,22 @@ int conv_candidates(const ConvArgs& a, ConvCfg* out, int cap) {
   int n = 0;
   const int nch = conv_nch(a);
   for (const auto& t : kTiles) {
-    for (int resw = 1; resw >= 0; --resw) {
-      int gbest = 0;
-      for (int G = nch; G >= 1 && !gbest; --G)
-        if (conv_cfg_ok(a, ConvCfg{t[0], t[1], G, resw, 1})) gbest = G;
-      if (!gbest) continue;
-      // persistent grid, and (for layers with few tiles) one block per tile
-      for (int persist = 1; persist >= 0; --persist) {
-        if (n < cap) out[n] = ConvCfg{t[0], t[1], gbest, resw, persist};
-        ++n;
-        if (!resw && gbest > 1) {
-          if (n < cap) out[n] = ConvCfg{t[0], t[1], 1, resw, persist};
+    for (int kind = 0; kind <= 2; kind += 2)  // 4- and 8-wave patch kernels
+      for (int resw = 1; resw >= 0; --resw) {
+        int gbest = 0;
+        for (int G = nch; G >= 1 && !gbest; --G)
+          if (conv_cfg_ok(a, ConvCfg{t[0], t[1], G, resw, 1, kind})) gbest = G;
+        if (!gbest) continue;
+        // persistent grid, and (for layers with few tiles) one block per tile
+        for (int persist = 1; persist >= 0; --persist) {
+          if (n < cap) out[n] = ConvCfg{t[0], t[1], gbest, resw, persist, kind};
           ++n;
+          if (!resw && gbest > 1) {
+            if (n < cap) out[n] = ConvCfg{t[0], t[1], 1, resw, persist, kind};
+            ++n;
+          }
         }
       }
-    }
     // 1x1 layers: the direct-B kernel
     for (int persist = 1; persist >= 0; --persist) {
       const ConvCfg d{t[0], t[1], 1, 1, persist, 1};

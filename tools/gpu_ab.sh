@@ -24,7 +24,7 @@ for rep in $(seq 1 "${REPS:-2}"); do
   done
 done
 [ "${PMC:-1}" = 1 ] || exit 0
-for v in ${VARIANTS:-base default}; do
+for v in ${PMC_VARIANTS:-${VARIANTS:-base default}}; do
   for c in FETCH_SIZE WRITE_SIZE; do
     RV_LIB_VARIANT=$v timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_${v}_$c" \
       -o pmc -- python3 tools/pmc_step.py > "$O/pmc_${v}_$c.log" 2>&1 || { tail "$O/pmc_${v}_$c.log"; exit 1; }

@@ -23,7 +23,13 @@ eng = RoadVisionEngine(bench.bench_config(), S, (1080, 1920), device=dev, pair=P
 frames = road_frames(S, 1 + P, 1080, 1920, device=dev)
 ts = torch.tensor([[f / 30.0] * S for f in range(1 + P)], dtype=torch.float64, device=dev)
 eng.step(frames[0], ts[0])
-eng.autotune(frames[0])  # the bench's kernel configurations (at the unit's batch)
+if os.environ.get("TUNE"):  # the configurations a bench run saved (--tune-save)
+    import json
+    eng.detector.load_tuned([tuple(c) for c in json.load(open(os.environ["TUNE"]))["configs"]])
+else:  # the bench's kernel configurations (at the unit's batch, persistent grids)
+    eng.autotune(frames[0])
+    eng.detector.load_tuned([tuple(c[:4]) + (1,) + tuple(c[5:])
+                             for c in eng.detector.tuned_configs()])
 if P > 1:
     from rvs_amd.handback import Record
     recs = [Record(S, eng.detector.max_det, dev) for _ in range(P)]
