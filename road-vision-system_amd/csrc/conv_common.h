@@ -1,0 +1,50 @@
+// Device helpers shared by the conv kernels (conv.hip) and the stem /
+// conv0 kernels (stem.hip): operand vector types, bf16 packing, SiLU, the
+// raw buffer-resource constants and the fp8 encoder.
+#pragma once
+#include "conv.h"
+
+namespace rv {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+typedef __attribute__((ext_vector_type(2))) float f32x2v;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
+typedef __attribute__((ext_vector_type(2))) unsigned int v2u32;
+
+// f32 -> bf16, round to nearest even, on the hardware converter
+// (v_cvt_pk_bf16_f32: two values per instruction).
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{lo, hi}, bf16x2v));
+}
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+// SiLU x * sigmoid(x) = x * 1/(1 + e^-x) with the hardware reciprocal
+// (<= 1 ulp f32; the result is stored as bf16).
+__device__ __forceinline__ float silu(float v) {
+  return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+}
+
+// Buffer-resource LDS-DMA (conv_patch_kernel): dword3 of the descriptor
+// for a raw (stride 0) buffer on gfx950, and the voffset that the range
+// check (voffset + soffset against num_records, checked on the GPU:
+// tools/probe_buffer_oob.hip) always rejects -- such a load writes zeros.
+constexpr int kRsrcFlags = 0x00020000;
+constexpr uint32_t kOOB = 0x80000000u;
+// fp8 epilogue8 (ConvArgs::in8): dequantise (acc * wscale[co] * s_in), bias,
+// SiLU, residual (fp8 code * s_res), then per output view fp8 codes of
+// value / s_out (v_cvt_pk_fp8_f32, round to nearest even, saturated to
+// +-448 first) or bf16 / f32.
+__device__ __forceinline__ uint32_t f8_encode4(const float (&v)[4], float inv_s) {
+  float q[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = fminf(fmaxf(v[i] * inv_s, -448.f), 448.f);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], w, true);
+  return (uint32_t)w;
+}
+
+}  // namespace rv

@@ -66,25 +66,30 @@ __device__ __forceinline__ int clahe_luma(int b, int g, int r) {
 
 // ---------------------------------------------------------------------------
 // Kernel A: per (tile, frame) histogram of Y -> clip -> redistribute -> LUT.
-// One 256-thread workgroup per tile.  16 LDS histogram copies, copy = lane
-// & 15 (shared by the 4 waves), copy-major with a 257-word stride: bin y of
-// copy c is word 257 c + y, bank (c + y) mod 64.  Equal Y values in a wave
-// (flat sky / asphalt) land on 16 different banks, with at most 2 lanes of
-// a 32-lane group on one address (lanes l, l + 16); nearby Y values in
-// different copies spread over the banks as well.  (r02/r03 used copy =
-// wave x lane & 3, bin-major: one wave reached only 16 banks and up to 16
-// lanes hit one address -- SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.78.
-// One copy per lane with packed u16 counters was measured slower: 47.5 vs
-// 42.2 us at 32 x 1080p, its 33 KB of LDS halves the resident blocks.)
+// One 256-thread workgroup per tile.
+// PACKED (every tile whose counts fit 16 bits; the default at 1080p): 32
+// LDS histogram copies, copy = lane & 31, two bins per word as u16 counts:
+// bin y of copy c is half y & 1 of word 32 (y >> 1) + c.  An atomic add's
+// bank is then (word mod 32/64) = c + 32 ((y >> 1) & 1): the 32 lanes of a
+// lane group always hit 32 different banks and never one address, whatever
+// the image -- conflict-free.  The reduction reads a row's 32 words as 8
+// rotated 16-B quads (conflict-free) and, for tiles below 2^16 pixels, adds
+// whole words before extracting the bin's half.  16 KB of LDS, as before.
+// Otherwise (tiles of > 2M pixels): 16 u32 copies, copy = lane & 15, word
+// 257 c + y.
+// (r02/r03: copy = wave x lane & 3, bin-major -- a wave reached only 16 banks
+// and up to 16 lanes hit one address, SQ_LDS_BANK_CONFLICT /
+// SQ_LDS_IDX_ACTIVE 0.78; the 257-word form alone: 0.68.  r02's one copy
+// per lane with u16 counters in 33 KB halved the resident blocks: slower.)
 // ---------------------------------------------------------------------------
-template <int SPACE>
+template <int SPACE, bool PACKED>
 __device__ __forceinline__ void clahe_lut_body(const uint8_t* __restrict__ in,
                                                uint8_t* __restrict__ lut, int H, int W, int pitch,
                                                const ClaheGeo& g, int tile, int b, int t) {
-  constexpr int kCopies = 16;
-  constexpr int kStride = 257;  // words per copy (odd: copy c shifts the banks by c)
-  constexpr int kWords = kStride * kCopies;
-  __shared__ int hist[kWords];
+  constexpr int kCopies = PACKED ? 32 : 16;
+  constexpr int kStride = PACKED ? 0 : 257;  // u32 form: words per copy
+  constexpr int kWords = PACKED ? 128 * 32 : kStride * kCopies;
+  __shared__ __attribute__((aligned(16))) int hist[kWords];
   __shared__ int wsum[4], wtot[4];
   const int wave = t >> 6;
   const int r_lo = 0, r_hi = g.th;
@@ -98,8 +103,13 @@ __device__ __forceinline__ void clahe_lut_body(const uint8_t* __restrict__ in,
   const bool inside = (x0 + g.tw <= W) && (y0 + g.th <= H);
   const bool vec = inside && (g.tw % 4 == 0) && (pitch % 4 == 0) &&
                    ((((uintptr_t)frame) + (uintptr_t)x0 * 3) % 4 == 0);
-  int* h = hist + (t & (kCopies - 1)) * kStride;  // bin y -> h[y]
-  auto bump = [&](int y) { atomicAdd(&h[y], 1); };
+  int* h = hist + (t & (kCopies - 1)) * (PACKED ? 1 : kStride);
+  auto bump = [&](int y) {
+    if constexpr (PACKED)
+      atomicAdd(&h[(y >> 1) * 32], 1 << ((y & 1) << 4));
+    else
+      atomicAdd(&h[y], 1);
+  };
   if (vec) {
     const int groups = g.tw >> 2;
     const int total = groups * (r_hi - r_lo);
@@ -147,8 +157,34 @@ __device__ __forceinline__ void clahe_lut_body(const uint8_t* __restrict__ in,
   __syncthreads();
 
   int v = 0;
+  if constexpr (PACKED) {
+    // bin t = half t & 1 of the 32 copies' words of row t >> 1, read as 8
+    // 16-B quads (quad j rotated by the row: lanes of one ds_read_b128 group
+    // cover 8 rows x 2 bin halves on 16 distinct bank slots)
+    const int rw = t >> 1, sh = (t & 1) << 4;
+    const uint4* row = (const uint4*)(hist + rw * 32);
+    if ((long)g.tw * g.th <= 65535) {
+      // the low halves' sum is the bin's count (<= tile pixels < 2^16): add
+      // whole words, extract once
+      uint32_t sum = 0;
 #pragma unroll
-  for (int c = 0; c < kCopies; ++c) v += hist[c * kStride + t];
+      for (int j = 0; j < 8; ++j) {
+        const uint4 q = row[(j + rw) & 7];
+        sum += q.x + q.y + q.z + q.w;
+      }
+      v = (int)((sum >> sh) & 0xFFFF);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint4 q = row[(j + rw) & 7];
+        v += (int)(((q.x >> sh) & 0xFFFF) + ((q.y >> sh) & 0xFFFF) + ((q.z >> sh) & 0xFFFF) +
+                   ((q.w >> sh) & 0xFFFF));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < kCopies; ++c) v += hist[c * kStride + t];
+  }
   if (g.clip_limit > 0) {
     int ex = v > g.clip_limit ? v - g.clip_limit : 0;
     v = v > g.clip_limit ? g.clip_limit : v;
@@ -180,17 +216,28 @@ __device__ __forceinline__ void clahe_lut_body(const uint8_t* __restrict__ in,
   dst[t] = (uint8_t)sat_u8(__float2int_rn(f));
 }
 
-template <int SPACE>
+template <int SPACE, bool PACKED>
 __global__ __launch_bounds__(256) void clahe_lut_kernel(const uint8_t* __restrict__ in,
                                                         uint8_t* __restrict__ lut, int H, int W,
                                                         int pitch, ClaheGeo g) {
-  clahe_lut_body<SPACE>(in, lut, H, W, pitch, g, blockIdx.x, blockIdx.y, threadIdx.x);
+  clahe_lut_body<SPACE, PACKED>(in, lut, H, W, pitch, g, blockIdx.x, blockIdx.y, threadIdx.x);
+}
+
+// u16 counts per (copy, bin) fit: a copy is shared by 8 threads (lanes c,
+// c + 32 of 4 waves), each bumping at most 4 ceil(tw/4 th / 256) (vector
+// path) or ceil(tw th / 256) pixels
+static bool clahe_packed_ok(const ClaheGeo& g) {
+  const long per_thread = 4L * (((long)(g.tw / 4) * g.th + 255) / 256) + ((long)g.tw * g.th + 255) / 256;
+  return 8 * per_thread <= 65535;
 }
 
 template <int SPACE>
 static void launch_clahe_lut(const uint8_t* in, uint8_t* lut, int B, int H, int W, int pitch,
                              const ClaheGeo& g, hipStream_t s) {
-  clahe_lut_kernel<SPACE><<<dim3(g.tiles * g.tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  if (clahe_packed_ok(g))
+    clahe_lut_kernel<SPACE, true><<<dim3(g.tiles * g.tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
+  else
+    clahe_lut_kernel<SPACE, false><<<dim3(g.tiles * g.tiles, B), 256, 0, s>>>(in, lut, H, W, pitch, g);
 }
 
 // CLAHE_Interpolation_Body per-axis coefficients.

@@ -626,7 +626,12 @@ struct Exec {
   // Two convs that share their input buffer, kernel size, stride and
   // activation and write adjacent channel slices of one output view -- the
   // Detect head's cv2 / cv3 branches -- as one grouped launch
-  // (ConvArgs::g2_*).  RV_HEAD_PAIR=0 launches them separately.
+  // (ConvArgs::g2_*).  Default: grouped in fp8 plans only.  bf16 plans launch
+  // the branches separately: with the 8-wave patch kernel each branch runs
+  // as ONE cout tile of its own width (box 64, class 80) reading the input
+  // once, where the grouped launch's 64-wide tiles padded the class branch
+  // to 128 (r04: P3 head 306 -> 260 us per 128-frame unit,
+  // profiles/r04/conv_table_eager_*).  RV_HEAD_PAIR=1 / 0 forces either.
   void conv_pair(const std::string& n1, View in1, const std::string& n2, View in2, int li,
                  View o0) {
     if (status) return;
@@ -635,7 +640,8 @@ struct Exec {
     const ConvSpec& c1 = M->def.convs[i1];
     const ConvSpec& c2 = M->def.convs[i2];
     const View o2{o0.buf, o0.cs, o0.co + c1.cout};
-    static const bool pair = !getenv("RV_HEAD_PAIR") || atoi(getenv("RV_HEAD_PAIR")) != 0;
+    static const int env = getenv("RV_HEAD_PAIR") ? atoi(getenv("RV_HEAD_PAIR")) : -1;
+    const bool pair = env >= 0 ? env != 0 : c1.f8;
     if (!pair || in1.buf != in2.buf || in1.cs != in2.cs || c1.k != c2.k || c1.s != c2.s ||
         c1.act != c2.act || c1.cout % 64 != 0) {
       conv(n1, in1, li, o0);
