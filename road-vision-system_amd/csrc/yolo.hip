@@ -664,6 +664,10 @@ struct Exec {
     launch(a, i1, fl);
   }
 
+  static bool c2f_will_fuse(int c, int n, bool fuse, int up0, View o1, View o0) {
+    return fuse && up0 == 0 && o1.buf < 0 && c2f_fusable(c, n, 2 * c, 0, o0.cs, o0.co);
+  }
+
   // C2f(prefix): in view (map li) -> concat buffer cb -> outputs.  With
   // `fuse`, narrow blocks run cv1 and then one fused launch for the
   // bottlenecks + cv2 (c2f.hip; intermediates stay in LDS).
@@ -671,10 +675,13 @@ struct Exec {
            int up0 = 0, View o1 = {-1, 0, 0}, int up1 = 0, bool fuse = false,
            bool cv1_done = false, const VIn* vin = nullptr) {
     const int c = c2 / 2;
-    const int cs = (2 + n) * c;
+    // a fused chain keeps z_i in LDS, so its concat buffer holds y0, y1
+    // only: pixel stride 2c (denser cv1 stores and chain reads)
+    const bool fused = c2f_will_fuse(c, n, fuse, up0, o1, o0);
+    const int cs = fused ? 2 * c : (2 + n) * c;
     if (!cv1_done)
       conv(p + ".cv1", in, li, View{cb, cs, 0}, 0, View{-1, 0, 0}, 0, View{-1, 0, 0}, vin);
-    if (fuse && !status && up0 == 0 && o1.buf < 0 && c2f_fusable(c, n, cs, 0, o0.cs, o0.co)) {
+    if (fused && !status) {
       Model::FusedC2f f;
       memset(&f.a, 0, sizeof(f.a));
       f.C = c;
@@ -699,15 +706,17 @@ struct Exec {
         f.a.wb[i] = wptr(cbv);
         f.a.bb[i] = bptr(cbv);
         // trace records keep the layer list complete (the buffers are not
-        // written: parity forwards run unfused)
+        // written: parity forwards run unfused; the records show the unfused
+        // concat layout)
         const int tmp = M->tmp_of(q);
-        const View bin{cb, cs, (1 + i) * c};
+        const int cs_u = (2 + n) * c;
+        const View bin{cb, cs_u, (1 + i) * c};
         const View none{-1, 0, 0};
         ConvArgs aa = args(ca, bin, li, View{tmp, c, 0}, 0, none, 0, none);
         trace(ia, aa, bin, View{tmp, c, 0}, 0, none, 0, none);
-        ConvArgs ab = args(cbv, View{tmp, c, 0}, li, View{cb, cs, (2 + i) * c}, 0, none, 0,
+        ConvArgs ab = args(cbv, View{tmp, c, 0}, li, View{cb, cs_u, (2 + i) * c}, 0, none, 0,
                            shortcut ? bin : none);
-        trace(ib, ab, View{tmp, c, 0}, View{cb, cs, (2 + i) * c}, 0, none, 0, shortcut ? bin : none);
+        trace(ib, ab, View{tmp, c, 0}, View{cb, cs_u, (2 + i) * c}, 0, none, 0, shortcut ? bin : none);
         flops += flops_of(ca, aa) + flops_of(cbv, ab);
       }
       const int i2 = spec(p + ".cv2");
@@ -718,8 +727,9 @@ struct Exec {
       f.a.out = (bf16_t*)ptr(o0.buf);
       f.a.out_cs = o0.cs;
       f.a.out_co = o0.co;
-      rec = args(c2s, View{cb, cs, 0}, li, o0, 0, View{-1, 0, 0}, 0, View{-1, 0, 0});
-      trace(i2, rec, View{cb, cs, 0}, o0, 0, View{-1, 0, 0}, 0, View{-1, 0, 0});
+      const int cs_u = (2 + n) * c;  // cv2's Cin: the unfused concat width
+      rec = args(c2s, View{cb, cs_u, 0}, li, o0, 0, View{-1, 0, 0}, 0, View{-1, 0, 0});
+      trace(i2, rec, View{cb, cs_u, 0}, o0, 0, View{-1, 0, 0}, 0, View{-1, 0, 0});
       flops += flops_of(c2s, rec);
       M->fused.push_back(f);
       rec.fused = (int)M->fused.size();
@@ -727,7 +737,7 @@ struct Exec {
       // every weight of the chain read once
       double wbytes = 0.0;
       for (int i = 0; i < n; ++i) wbytes += 2.0 * 2 * 9 * c * 32;
-      wbytes += 2.0 * c2 * ((cs + 31) / 32 * 32);
+      wbytes += 2.0 * c2 * ((cs_u + 31) / 32 * 32);
       fused_bytes = (double)B * f.a.H * f.a.W * (2.0 * c * 2 + 2.0 * c2) + wbytes;
       launch(rec, i2, flops);
       return;
@@ -1035,7 +1045,9 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
   // the fused stem also runs model.2.cv1 (32 -> 32 1x1) from its registers
   // into the model.2 concat buffer when the shapes allow
   const int i2cv1 = M->def.find("model.2.cv1");
-  const int c2cs = (2 + v.nb) * (v.c2 / 2);
+  const int c2cs = E.c2f_will_fuse(v.c2 / 2, v.nb, fuse_c2f, 0, View{-1, 0, 0}, View{M->X2, v.c2, 0})
+                       ? v.c2
+                       : (2 + v.nb) * (v.c2 / 2);
   const bool stem_cv1 = fuse_stem && i2cv1 >= 0 && M->def.convs[i2cv1].cin == 32 &&
                         M->def.convs[i2cv1].cout == 32 && M->def.convs[i2cv1].k == 1;
   if (fuse_stem) {

@@ -59,13 +59,18 @@ class Introspect:
             self.lib.rv_yolo_buffer_info(eng._h, B, i, info, ctypes.byref(off))
             self.bufs.append((info[0], info[1], info[2], info[3], off.value))
 
-    def raw_u16(self, buf):
+    def raw_u16(self, buf, cs=None):
         h, w, c, f32, off = self.bufs[buf]
+        c = cs or c
         n = self.B * h * w * c
         return self.ws[off:off + 2 * n].view(np.uint16).reshape(self.B, h, w, c)
 
-    def view(self, buf):
+    def view(self, buf, cs=None):
+        """`cs`: the channel stride a forward actually used (a fused C2f
+        chain's concat buffer holds y0, y1 only: stride 2c in the same
+        allocation)."""
         h, w, c, f32, off = self.bufs[buf]
+        c = cs or c
         n = self.B * h * w * c
         if f32:
             return self.ws[off:off + 4 * n].view(np.float32).reshape(self.B, h, w, c)
@@ -229,7 +234,7 @@ def test_fused_stem_matches_unfused(cuda):
     ins = Introspect(eng, B)
     x1_fused = ins.view(1).copy()
     c2 = [i for i, bb in enumerate(ins.bufs) if bb[2] == 48 and bb[0] == 96][0]
-    cv1_fused = ins.view(c2)[..., :32].copy()
+    cv1_fused = ins.view(c2, cs=32).copy()  # fused model.2: [y0 | y1] only
     raw = torch.empty((B, 84, eng.A), dtype=torch.float32, device=cuda)
     eng.forward_raw(lb, raw)  # raw output requested: conv0 + model.1 separately
     ins2 = Introspect(eng, B)
@@ -277,7 +282,7 @@ def test_stem_cv1_bit_identical_to_unfused_1x1(cuda):
     ins = Introspect(eng, B)
     x1_f = ins.raw_u16(1).copy()
     c2 = [i for i, bb in enumerate(ins.bufs) if bb[2] == 48 and bb[0] == 96][0]
-    cv1_f = ins.raw_u16(c2)[..., :32].copy()
+    cv1_f = ins.raw_u16(c2, cs=32).copy()  # fused model.2: [y0 | y1] only
     raw = torch.empty((B, 84, eng.A), dtype=torch.float32, device=cuda)
     eng.forward_raw(lb, raw)
     ins2 = Introspect(eng, B)
