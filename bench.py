@@ -25,6 +25,7 @@ scaling); rank timings are reduced with a MAX (rvs_amd.shard.timed_job).
 Prints ONE JSON line (rank 0).
 """
 import argparse
+import gc
 import hashlib
 import importlib
 import json
@@ -247,8 +248,25 @@ class BenchJob:
             # device-only rerun), so every timed run sees exactly the tracks
             # the warm-up steps left
             self.sort_saved = eng.tracker.state[0].clone()
+            # everything allocated so far (torch, the engine, the plans) is
+            # long-lived: move it out of the collector's generations, so a
+            # full collection triggered by the consumer's Detection objects
+            # does not traverse it inside a timed region (a 75 ms stall in
+            # one of six runs without this, tools/consumer_ab.py); done
+            # before the warm runs, so the device is busy up to the region
+            gc.collect()
+            gc.freeze()
+            # the warm runs are the timed region's code path (schedule, the
+            # consumer or watcher thread, its hand-back waits and Detection
+            # lists), under their own marker tags 9/10: without the host
+            # thread in them, its first-run costs landed in the timed region
+            # (first run 40.0-40.3k against 41.7-41.8k frames/s after one
+            # more untimed run with the thread, tools/consumer_ab.py, r04)
+            tags, self.tags = self.tags, (9, 10)
             for _ in range(a.warm_runs):
-                self.runner.run()
+                self.run()
+                self.sync()
+            self.tags = tags
             eng.tracker.state[0].copy_(self.sort_saved)
         torch.cuda.synchronize()
 

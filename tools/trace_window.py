@@ -9,7 +9,7 @@ marker of tag A and the first marker of tag B after it.  rv_trace_marker
 launches `tag` workgroups of 64, so a dispatch's tag is Grid_Size_X / 64.
 bench.py's tags: 1,2 the timed region; 3,4 the in-pipeline conv profiling
 pass; 5,6 the eager conv profiling pass (5 repetitions of every launch);
-7,8 the device-only rerun of the timed region.
+7,8 the device-only rerun of the timed region; 9,10 each warm run before it.
 writes OUT_PREFIX_kernel_stats.csv (rocprofv3 --stats columns) and
 OUT_PREFIX_summary.txt (per-step time of each kernel family, conv family
 included, and the window's wall time)."""
