@@ -879,6 +879,18 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
         px[n] = tx * g.C + ocol[n];
         pv[n] = oin[n] && py[n] < a.Ho && px[n] < a.Wo;
       }
+#ifdef RV_EPI_SKIP
+      if (a.Cout == 12345) {  // timing experiment: keep the MFMAs live, skip the epilogue
+        float t = 0.f;
+#pragma unroll
+        for (int m = 0; m < MR; ++m)
+#pragma unroll
+          for (int n = 0; n < NR; ++n) t += acc[m][n][0] + acc[m][n][3];
+        ((float*)a.out0)[tid] = t;
+      }
+      if (true) {
+      } else
+#endif
       if constexpr (F8) {
         epilogue8<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias, dq);
       } else if (g.fast) {
