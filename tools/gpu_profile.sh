@@ -16,9 +16,11 @@ ST=$(find "$OUT/raw" -name "*kernel_stats.csv" | head -1)
 cp "$ST" "$OUT/rocprof_kernel_stats_whole_run.csv"
 python3 tools/trace_window.py "$KT" "$STEPS" "$OUT/timed" || exit $?
 python3 tools/stream_busy.py "$KT" "$STEPS" > "$OUT/timed_streams.txt" || exit $?
+python3 tools/timeline.py "$KT" 1,2 250 > "$OUT/timed_timeline.txt" || exit $?
 if grep -q "device-only" "$OUT/bench_profiled.json" 2>/dev/null; then  # the device-only rerun
   python3 tools/trace_window.py "$KT" "$STEPS" "$OUT/devonly" 7,8 > /dev/null || exit $?
   python3 tools/stream_busy.py "$KT" "$STEPS" 7,8 > "$OUT/devonly_streams.txt" || exit $?
+  python3 tools/timeline.py "$KT" 7,8 250 > "$OUT/devonly_timeline.txt" || exit $?
 fi
 if [ "${CONV_TIMING:-none}" = both ]; then  # the conv profiling passes' windows
   python3 tools/trace_window.py "$KT" "$STEPS" "$OUT/convpass_pipeline" 3,4 > /dev/null || exit $?
