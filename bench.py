@@ -270,11 +270,18 @@ class BenchJob:
             eng.tracker.state[0].copy_(self.sort_saved)
         torch.cuda.synchronize()
 
-    def _consume(self, wait_step, materialise: bool):
+    def _consume(self, wait_step, materialise: bool, ready=None):
         """The consumer: every step's List[Detection] per stream, built as
         soon as that step's record has been handed back (materialise=False:
         only the host time each step became available)."""
+        from rvs_amd.handback import DetectionPool
         names, n_det, busy, done = self.eng.names, 0, 0.0, []
+        # Detection shells made while waiting for the next hand-back (the
+        # allocations move out of the step's critical tail; DESIGN.md §5)
+        # (made only while the next step is not ready yet: in a burst of
+        # hand-backs the lists are built from what the pool holds)
+        pool = DetectionPool() if materialise and ready is not None else None
+        want = 8192
         # A/B probes: RV_CONSUMER_DEFER=1 builds every list after the last
         # step's hand-back (still inside the timed region); RV_CONSUMER_NOGC=1
         # keeps the garbage collector off while the lists are built
@@ -286,11 +293,16 @@ class BenchJob:
         if defer:
             wait_step(len(self.records) - 1)
         for k, rec in enumerate(self.records):
+            if pool is not None:
+                while len(pool.items) < want and not ready(k):
+                    pool.top_up(min(want, len(pool.items) + 512))
             wait_step(k)
             t = time.perf_counter()
             done.append(t)
             if materialise:
-                n_det += sum(len(x) for x in rec.detections(names))
+                nk = sum(len(x) for x in rec.detections(names, pool))
+                n_det += nk
+                want = max(want, 5 * nk)
                 busy += time.perf_counter() - t
         if nogc:
             gc.enable()
@@ -305,6 +317,7 @@ class BenchJob:
         if self.runner is not None:
             self.runner.run()
             wait = self.runner.wait_step
+            ready = self.runner.step_ready
         else:
             evs = []
             for k in range(self.K):
@@ -313,11 +326,12 @@ class BenchJob:
                 e.record()
                 evs.append(e)
             wait = lambda k: evs[k].synchronize()  # noqa: E731
+            ready = lambda k: evs[k].query()  # noqa: E731
         self.issue_s = time.perf_counter() - t0
         _lib.call("rv_trace_marker", self.tags[1], st)
         if self.consume != "off":
             self._consumer = threading.Thread(target=self._consume,
-                                              args=(wait, self.consume == "consume"))
+                                              args=(wait, self.consume == "consume", ready))
             self._consumer.start()
 
     def sync(self):

@@ -528,6 +528,9 @@ int rv_sched_num_nodes(void* handle);
  * before the first run, while a run is issuing, after a run that failed
  * part-way, or for an event the latest run did not issue. */
 int rv_sched_event_sync(void* handle, int event);
+/* Non-blocking form: 1 = completed, 0 = not yet, < 0 = error (same
+ * validity rule as rv_sched_event_sync). */
+int rv_sched_event_query(void* handle, int event);
 /* Milliseconds between two timing record nodes of the last run (same
  * validity rule as rv_sched_event_sync). */
 int rv_sched_event_elapsed(void* handle, int a, int b, float* ms);

@@ -16,6 +16,13 @@
  *   record: a buffer (the pinned host record), names: list of class names,
  *   cls: the Detection class.  -1 track ids and NaN metrics become None,
  *   class ids outside names become str(id) -- as the Python version.
+ * shells(cls, n) -> list of n Detection objects whose 10 fields are None
+ * build(record, S, dmax, names, cls, pool) -- the same lists, but each
+ *   Detection is taken from the end of `pool` (a list of shells, consumed)
+ *   and its fields are set in place; a fresh one is made when the pool runs
+ *   out.  Object and attribute-dict allocation then happen when the shells
+ *   are made -- by a consumer while it waits for the next hand-back --
+ *   instead of after the hand-back (a third less work after it).
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
@@ -33,10 +40,57 @@ static PyObject* k_names[10];
 static const char* k_fields[10] = {"x1",     "y1",       "x2",       "y2",         "conf",
                                    "cls_id", "cls_name", "track_id", "distance_m", "speed_kmh"};
 
+/* a Detection whose 10 fields are None (a dataclass instance: its type's
+   allocation plus an attribute dict) */
+static PyObject* new_shell(PyTypeObject* tp) {
+  PyObject* d = _PyDict_NewPresized(10);
+  if (!d) return NULL;
+  for (int f = 0; f < 10; ++f)
+    if (PyDict_SetItem(d, k_names[f], Py_None) < 0) {
+      Py_DECREF(d);
+      return NULL;
+    }
+  PyObject* obj = tp->tp_alloc(tp, 0);
+  if (!obj || PyObject_GenericSetDict(obj, d, NULL) < 0) {
+    Py_XDECREF(obj);
+    Py_DECREF(d);
+    return NULL;
+  }
+  Py_DECREF(d);
+  return obj;
+}
+
+static PyObject* shells(PyObject* self, PyObject* args) {
+  PyObject* cls;
+  Py_ssize_t n;
+  if (!PyArg_ParseTuple(args, "On", &cls, &n)) return NULL;
+  if (!PyType_Check(cls)) {
+    PyErr_SetString(PyExc_TypeError, "cls must be the Detection class");
+    return NULL;
+  }
+  if (n < 0) n = 0;
+  PyObject* out = PyList_New(n);
+  if (!out) return NULL;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* o = new_shell((PyTypeObject*)cls);
+    if (!o) {
+      Py_DECREF(out);
+      return NULL;
+    }
+    PyList_SET_ITEM(out, i, o);
+  }
+  return out;
+}
+
 static PyObject* build(PyObject* self, PyObject* args) {
-  PyObject *rec_obj, *names, *cls;
+  PyObject *rec_obj, *names, *cls, *pool = NULL;
   Py_ssize_t S, dmax;
-  if (!PyArg_ParseTuple(args, "OnnOO", &rec_obj, &S, &dmax, &names, &cls)) return NULL;
+  if (!PyArg_ParseTuple(args, "OnnOO|O", &rec_obj, &S, &dmax, &names, &cls, &pool)) return NULL;
+  if (pool == Py_None) pool = NULL;
+  if (pool && !PyList_Check(pool)) {
+    PyErr_SetString(PyExc_TypeError, "pool must be a list of Detection shells");
+    return NULL;
+  }
   if (!PyType_Check(cls)) {
     PyErr_SetString(PyExc_TypeError, "cls must be the Detection class");
     return NULL;
@@ -57,6 +111,8 @@ static PyObject* build(PyObject* self, PyObject* args) {
   const Row* rows = (const Row*)((const char*)buf.buf + hdr);
   PyTypeObject* tp = (PyTypeObject*)cls;
   const Py_ssize_t nn = PyList_GET_SIZE(names);
+  Py_ssize_t np = pool ? PyList_GET_SIZE(pool) : 0;  // shells left (taken from the end)
+  const Py_ssize_t np0 = np;
   PyObject* out = PyList_New(S);
   if (!out) goto fail;
   for (Py_ssize_t s = 0; s < S; ++s) {
@@ -103,15 +159,26 @@ static PyObject* build(PyObject* self, PyObject* args) {
       } else {
         v[9] = PyFloat_FromDouble(r->speed);
       }
-      PyObject* d = _PyDict_NewPresized(10);
-      PyObject* obj = tp->tp_alloc(tp, 0);
-      int bad = !d || !obj;
+      PyObject* obj;
+      PyObject* d;
+      int bad;
+      if (np > 0) {  // a shell: its dict already holds the 10 keys
+        obj = PyList_GET_ITEM(pool, np - 1);
+        Py_INCREF(obj);
+        --np;
+        d = PyObject_GenericGetDict(obj, NULL);
+        bad = !d;
+      } else {
+        d = _PyDict_NewPresized(10);
+        obj = tp->tp_alloc(tp, 0);
+        bad = !d || !obj;
+        if (!bad && PyObject_GenericSetDict(obj, d, NULL) < 0) bad = 1;
+      }
       for (int f = 0; f < 10; ++f) {
         if (!v[f]) bad = 1;
         if (!bad && PyDict_SetItem(d, k_names[f], v[f]) < 0) bad = 1;
         Py_XDECREF(v[f]);
       }
-      if (!bad && PyObject_GenericSetDict(obj, d, NULL) < 0) bad = 1;
       Py_XDECREF(d);
       if (bad) {
         Py_XDECREF(obj);
@@ -120,9 +187,11 @@ static PyObject* build(PyObject* self, PyObject* args) {
       PyList_SET_ITEM(lst, i, obj);
     }
   }
+  if (pool && np < np0 && PyList_SetSlice(pool, np, np0, NULL) < 0) goto fail;
   PyBuffer_Release(&buf);
   return out;
 fail:
+  if (pool && np < np0) PyList_SetSlice(pool, np, np0, NULL);
   PyBuffer_Release(&buf);
   Py_XDECREF(out);
   if (!PyErr_Occurred()) PyErr_NoMemory();
@@ -131,7 +200,8 @@ fail:
 
 static PyMethodDef methods[] = {
     {"build", build, METH_VARARGS,
-     "build(record, S, dmax, names, Detection) -> S lists of Detection"},
+     "build(record, S, dmax, names, Detection[, pool]) -> S lists of Detection"},
+    {"shells", shells, METH_VARARGS, "shells(Detection, n) -> n Detection objects, fields None"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_rvhandback",

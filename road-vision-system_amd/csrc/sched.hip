@@ -255,6 +255,22 @@ extern "C" int rv_sched_event_sync(void* handle, int event) {
   }
 }
 
+// Non-blocking: 1 if the last run's record node `event` has completed, 0 if
+// not yet (same validity rule as rv_sched_event_sync), so a consumer can do
+// other work -- e.g. prepare the objects it will fill -- while it waits.
+extern "C" int rv_sched_event_query(void* handle, int event) {
+  RV_CHECK_ARG(handle != nullptr, "null handle");
+  Schedule* S = static_cast<Schedule*>(handle);
+  RV_CHECK_ARG(event >= 0 && event < (int)S->events.size(), "rv_sched_event_query: event %d", event);
+  const int64_t g = S->done_gen.load();
+  RV_CHECK_ARG(g >= 0 && S->ev_gen[event] == g,
+               "rv_sched_event_query: event %d was not issued by the latest completed run", event);
+  const hipError_t e = hipEventQuery(S->events[event]);
+  if (e == hipSuccess) return 1;
+  if (e == hipErrorNotReady) return 0;
+  return hip_check(e, "rv_sched hipEventQuery");
+}
+
 // Milliseconds between two timing record nodes of the last run.
 extern "C" int rv_sched_event_elapsed(void* handle, int a, int b, float* ms) {
   RV_CHECK_ARG(handle != nullptr && ms != nullptr, "null pointer");

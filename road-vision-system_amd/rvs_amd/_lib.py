@@ -128,6 +128,7 @@ _SIGS = {
                                 c_size_t, c_void_p]),
     "rv_sched_add_record": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "rv_sched_event_sync": (c_int, [c_void_p, c_int]),
+    "rv_sched_event_query": (c_int, [c_void_p, c_int]),
     "rv_sched_event_elapsed": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "rv_sched_add_wait": (c_int, [c_void_p, c_void_p, c_int]),
     "rv_sched_num_nodes": (c_int, [c_void_p]),
@@ -195,7 +196,7 @@ _RECORDABLE = {"rv_clahe_median_letterbox_u8", "rv_clahe_median_u8", "rv_letterb
                "rv_yolo_forward_part", "rv_nms_postprocess", "rv_sort_update",
                "rv_results_handback"}
 
-_NOCHECK = {"rv_sched_num_nodes", "rv_abi_version", "rv_cand_segments", "rv_yolo_cand_segments", "rv_clahe_median_fits", "rv_clahe_median_letterbox_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
+_NOCHECK = {"rv_sched_num_nodes", "rv_sched_event_query", "rv_abi_version", "rv_cand_segments", "rv_yolo_cand_segments", "rv_clahe_median_fits", "rv_clahe_median_letterbox_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
             "rv_yolo_num_buffers", "rv_yolo_trace", "rv_yolo_profile_read", "rv_yolo_tuned_config",
             "rv_yolo_profile_bytes", "rv_yolo_profile_times", "rv_yolo_buffer_esize", "rv_yolo_conv_candidates"}
 

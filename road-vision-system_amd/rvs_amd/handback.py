@@ -46,13 +46,33 @@ class Record:
         self.host = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True) if host else None
         self.seq = 0  # hand-backs issued into this record (RoadVisionEngine.results checks it)
 
-    def detections(self, names: Sequence[str]) -> List[List[Detection]]:
+    def detections(self, names: Sequence[str], pool: "DetectionPool" = None) -> List[List[Detection]]:
         """The reference's Detection lists of this record (the caller must
         have synchronised the stream that filled it): built in C
-        (_rvhandback) when available, else by to_detections."""
+        (_rvhandback) when available, else by to_detections.  With a `pool`,
+        the objects are taken from its pre-made shells (DetectionPool)."""
         if _rvhandback is not None:
-            return _rvhandback.build(self.host.numpy(), self.S, self.dmax, list(names), Detection)
+            return _rvhandback.build(self.host.numpy(), self.S, self.dmax, list(names), Detection,
+                                     pool.items if pool is not None else None)
         return to_detections(*self.arrays(), names)
+
+
+class DetectionPool:
+    """Pre-made Detection objects (every field None) for Record.detections:
+    a consumer tops the pool up while it waits for the next hand-back, so
+    the object and attribute-dict allocations are done before the record
+    arrives and only the field values are set after it.  The objects handed
+    out are ordinary Detection instances (equal to Detection(...) ones)."""
+
+    def __init__(self):
+        self.items: list = []
+
+    def top_up(self, n: int) -> None:
+        """Make shells until the pool holds at least n (no-op without the C
+        builder)."""
+        k = int(n) - len(self.items)
+        if k > 0 and _rvhandback is not None:
+            self.items.extend(_rvhandback.shells(Detection, k))
 
     def arrays(self):
         """(counts (S,), rows (S, dmax) structured) views of the host record.

@@ -129,6 +129,13 @@ class Schedule:
         """Block this thread until record node `event` of the last run()."""
         _lib.call("rv_sched_event_sync", self.h, int(event))
 
+    def event_query(self, event: int) -> bool:
+        """True once record node `event` of the last run() has completed
+        (non-blocking)."""
+        st = _lib.call("rv_sched_event_query", self.h, int(event))
+        _lib.check(0 if st >= 0 else st, "rv_sched_event_query")
+        return st == 1
+
     def elapsed_ms(self, a: int, b: int) -> float:
         ms = ctypes.c_float()
         _lib.call("rv_sched_event_elapsed", self.h, int(a), int(b), ctypes.byref(ms))
@@ -345,6 +352,14 @@ class PipelinedRun:
             self.sched.event_sync(e)
         else:
             e.synchronize()
+
+    def step_ready(self, k: int) -> bool:
+        """True once step k of the last run() has handed its results back
+        (non-blocking form of wait_step)."""
+        e = self._events.ev[("done", k)]
+        if self.sched is not None:
+            return self.sched.event_query(e)
+        return e.query()
 
     def step_done_ms(self) -> List[float]:
         """Completion time of every step of the last run, in ms after step

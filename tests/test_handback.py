@@ -90,3 +90,41 @@ def test_c_builder_matches_python():
     import pytest
     with pytest.raises(ValueError):
         handback._rvhandback.build(np.zeros(10, np.uint8), 2, 2, list(COCO80), Detection)
+
+
+def test_c_builder_pool_shells():
+    """Record.detections with a DetectionPool: the objects come from the
+    pool's pre-made shells (consumed from its end; fresh ones once it runs
+    out) and are exactly the objects of the plain build -- same fields,
+    types and field order -- so a consumer may make them ahead of a
+    hand-back (bench.py)."""
+    from rvs_amd import handback
+    assert handback._rvhandback is not None, "the C builder is not built (make -C csrc)"
+    rng = np.random.default_rng(12)
+    S, dmax = 6, 20
+    rows = np.zeros((S, dmax), ROW)
+    for f in ("x1", "y1", "x2", "y2", "conf"):
+        rows[f] = rng.uniform(-5, 2000, (S, dmax)).astype(np.float32)
+    rows["cls"] = rng.integers(-2, 84, (S, dmax))
+    rows["track_id"] = rng.integers(-1, 40, (S, dmax))
+    rows["dist"] = np.where(rng.random((S, dmax)) < 0.3, np.nan, rng.uniform(0, 9, (S, dmax)))
+    rows["speed"] = np.where(rng.random((S, dmax)) < 0.5, np.nan, rng.uniform(0, 9, (S, dmax)))
+    n = np.array([3, 0, 20, 7, -1, 25], np.int32)  # 50 detections
+    rec = _record_bytes(n, rows)
+    want = to_detections(n, rows, COCO80)
+    for size in (0, 10, 50, 80):
+        pool = handback.DetectionPool()
+        pool.top_up(size)
+        assert len(pool.items) == size
+        assert all(isinstance(o, Detection) and list(vars(o)) == list(vars(want[0][0]))
+                   and all(v is None for v in vars(o).values()) for o in pool.items)
+        spare = list(pool.items[:max(0, size - 50)])
+        got = handback._rvhandback.build(rec, S, dmax, list(COCO80), Detection, pool.items)
+        assert got == want
+        for a, b in zip(sum(got, []), sum(want, [])):
+            assert vars(a) == vars(b) and list(vars(a)) == list(vars(b))
+            assert all(type(getattr(a, f)) is type(getattr(b, f)) for f in vars(b))
+        assert len(pool.items) == max(0, size - 50)
+        assert all(x is y for x, y in zip(pool.items, spare))  # untouched shells stay
+        ids = {id(o) for o in sum(got, [])}
+        assert len(ids) == 50  # no object handed out twice
