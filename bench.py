@@ -280,7 +280,8 @@ class BenchJob:
         # allocations move out of the step's critical tail)
         # (made only while the next step is not ready yet: in a burst of
         # hand-backs the lists are built from what the pool holds)
-        pool = DetectionPool() if materialise and ready is not None else None
+        use_pool = os.environ.get("RV_CONSUMER_POOL", "1") != "0"  # A/B probe
+        pool = DetectionPool() if materialise and ready is not None and use_pool else None
         want = 8192
         # A/B probes: RV_CONSUMER_DEFER=1 builds every list after the last
         # step's hand-back (still inside the timed region); RV_CONSUMER_NOGC=1
@@ -712,21 +713,32 @@ def _stub_main(args, rank, world) -> None:
 
 def pair1_rate(job, rank: int, dev) -> dict:
     """The config's literal batch: one YOLOv8n forward per 32-stream step
-    (pipeline units of 1 step, autotuned at batch 32, the same K steps and
-    frames, the Detection consumer on), timed like the headline."""
-    from rvs_amd.shard import timed_job
-    a = argparse.Namespace(**vars(job.args))
-    a.pair, a.units, a.warm_runs, a.tune_load, a.tune_save = 1, "even", 1, None, None
-    j1 = BenchJob(a, rank, dev, frames=job.frames)
-    j1.warmup()
-    j1.prepare()
-    t = timed_job(j1.run, j1.sync, j1.units, dev)
-    j1.eng.close()
-    return {"value": round(t["value"], 2), "ms_per_step": round(t["elapsed_s"] / j1.K * 1e3, 4),
-            "forward_batch": j1.S,
+    (pipeline units of 1 step, autotuned at batch 32, the same K steps,
+    synthetic frames and consumer), timed like the headline -- in a fresh
+    child process (not exec'd: started as a child, its JSON line read back).
+    In this process a second engine's pipeline streams would share the
+    hardware queues with the first engine's (GPU_MAX_HW_QUEUES = 4): that
+    leg measured 27.8-33.6k frames/s against 36.5-37.1k for the same
+    configuration run alone (r04)."""
+    a = job.args
+    cmd = [sys.executable, os.path.abspath(__file__), "--steps", str(job.K), "--warmup", str(job.Wm),
+           "--pair", "1", "--units", "even", "--no-secondary", "--no-cpu-baseline",
+           "--conv-timing", "none", "--streams", str(job.S), "--gpus", "1"]
+    if a.exec_mode != "native":
+        cmd += ["--exec", a.exec_mode]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+                        "MASTER_PORT", "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID")}
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"pair-1 child exited {r.returncode}: {r.stderr[-800:]}")
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    return {"value": d["value"], "ms_per_step": d["ms_per_step"],
+            "device_only": (d.get("device_only") or {}).get("value"),
+            "forward_batch": job.S,
             "note": "pipeline units of 1 step: one forward over the step's 32 frames (the "
                     "config's batch=32), conv kernels autotuned at batch 32; same K steps, "
-                    "frames and consumer as the headline"}
+                    "synthetic frames and consumer as the headline; a fresh child process"}
 
 
 def secondary_legs(job, dev) -> dict:
