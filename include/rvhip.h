@@ -223,7 +223,10 @@ int rv_yolo_forward(void* handle, const uint8_t* lb, int B, void* ws, size_t ws_
  * only with part 0 = the whole forward).  Part 2 needs a part 0 or part 1
  * forward of the same handle before it (launch numbering of the autotuned
  * configurations).  With two handles + workspaces a pipelined caller runs
- * part 2 of step j-1 beside part 1 of step j. */
+ * part 2 of step j-1 beside part 1 of step j.  Part 1 itself may run as
+ * part 3 (the stem and model.2, lb used) then part 4 (model.3 .. model.15,
+ * lb unused; it must continue the handle's last part 3 with the same B and
+ * workspace), so a caller can order other work after the stem. */
 int rv_yolo_forward_part(void* handle, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
                          float* raw_out, float conf, void* cand, int cand_cap, int* cand_n,
                          void* stream, int part);

@@ -326,6 +326,9 @@ struct Model {
   // forward parts (rv_yolo_forward_part): launch index base of this call
   // (part 2 continues part 1's launch numbering) and part 1's launch count
   int li_base = 0, n_part1 = -1;
+  int n_part1a = -1;               // launches of the last part 3 (stem .. model.2)
+  int part1a_B = 0;
+  void* part1a_ws = nullptr;
   int part1_B = 0;                // batch and workspace of the last part 0 / part 1 forward:
   const void* part1_ws = nullptr;  // part 2 must continue exactly that forward
   // fp8 plans: per-buffer activation scales (value = code * scale), powers
@@ -986,15 +989,20 @@ extern "C" int rv_yolo_forward(void* h, const uint8_t* lb, int B, void* ws, size
 extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws, size_t ws_bytes,
                                     float* raw_out, float conf, void* cand, int cand_cap,
                                     int* cand_n, void* stream, int part) {
-  RV_CHECK_ARG(h && ws && (lb || part == 2), "null pointer");
-  RV_CHECK_ARG(part >= 0 && part <= 2, "part %d not in {0, 1, 2}", part);
+  RV_CHECK_ARG(h && ws && (lb || part == 2 || part == 4), "null pointer");
+  RV_CHECK_ARG(part >= 0 && part <= 4, "part %d not in {0, 1, 2, 3, 4}", part);
   Model* M = (Model*)h;
+  RV_CHECK_ARG(part != 4 || M->n_part1a >= 0, "forward part 4 before any part 3 of this handle");
+  RV_CHECK_ARG(part != 4 || (B == M->part1a_B && ws == M->part1a_ws),
+               "forward part 4 (B=%d, ws %p) does not continue the last part 3 of this handle "
+               "(B=%d, ws %p)", B, ws, M->part1a_B, M->part1a_ws);
   RV_CHECK_ARG(part != 2 || M->n_part1 >= 0,
                "forward part 2 before any part 0 / part 1 forward of this handle");
   RV_CHECK_ARG(part != 2 || (B == M->part1_B && ws == M->part1_ws),
                "forward part 2 (B=%d, ws %p) does not continue the last part 1 of this handle "
                "(B=%d, ws %p)", B, ws, M->part1_B, M->part1_ws);
-  RV_CHECK_ARG(part != 1 || !raw_out, "raw_out needs the whole forward (part 0)");
+  RV_CHECK_ARG((part != 1 && part != 3 && part != 4) || !raw_out,
+               "raw_out needs the whole forward (part 0)");
   RV_CHECK_ARG(B > 0 && B <= M->max_B, "B=%d outside (0, %d]", B, M->max_B);
   RV_CHECK_ARG(ws_bytes >= M->ws_bytes(B), "workspace %zu < %zu bytes", ws_bytes, M->ws_bytes(B));
   RV_CHECK_ARG(!cand || (cand_n && cand_cap > 0), "candidate buffers incomplete");
@@ -1014,7 +1022,7 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
   M->trace.clear();
   M->launches.clear();
   M->fused.clear();
-  M->li_base = part == 2 ? M->n_part1 : 0;
+  M->li_base = part == 2 ? M->n_part1 : (part == 4 ? M->n_part1a : 0);
   // fused C2f chains (c2f.hip) unless a raw parity forward keeps every
   // activation (RV_YOLO_OPT_RAW_UNFUSED) or RV_FUSE_C2F=0
   static const bool c2f_env = !getenv("RV_FUSE_C2F") || atoi(getenv("RV_FUSE_C2F")) != 0;
@@ -1030,6 +1038,7 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
             cat17 = v.h15 + v.h12;
   int st;
   if (part != 2) {
+  if (part != 4) {  // part 4 continues after model.2
   // backbone
   const ConvSpec& c0 = M->def.convs[0];
   const uint8_t* qb = M->dev + M->def.q_off;
@@ -1101,6 +1110,14 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
   }
   E.c2f("model.2", View{M->X1, v.c2, 0}, 2, M->C2, v.c2, v.nb, true, View{M->X2, v.c2, 0}, 0,
         View{-1, 0, 0}, 0, fuse_c2f, stem_cv1);
+  if (E.status) return E.status;
+  if (part == 3) {  // the stem and model.2: the VALU-heavy start of part 1
+    M->n_part1a = M->li_base + (int)M->launches.size();
+    M->part1a_B = B;
+    M->part1a_ws = ws;
+    return RV_OK;
+  }
+  }  // part != 4
   E.conv("model.3", View{M->X2, v.c2, 0}, 2, View{M->X3, v.c3, 0});
   E.c2f("model.4", View{M->X3, v.c3, 0}, 3, M->C4, v.c3, v.nm, true,
         View{M->CAT14, cat14, v.h12}, 0, View{-1, 0, 0}, 0, v.c3 / 2 == 16 ? fuse_c2f : fuse_c2f32);
@@ -1137,10 +1154,10 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
         View{M->X15, v.h15, 0}, 0, View{-1, 0, 0}, 0, v.h15 / 2 == 16 ? fuse_c2f : fuse_c2f32,
         false, vcat ? &vin15 : nullptr);
   if (E.status) return E.status;
-  M->n_part1 = (int)M->launches.size();
+  M->n_part1 = M->li_base + (int)M->launches.size();
   M->part1_B = B;
   M->part1_ws = ws;
-  if (part == 1) return RV_OK;
+  if (part == 1 || part == 4) return RV_OK;
   }  // part != 2
   // Detect head of level i: box (cv2) and class (cv3) branches, one grouped
   // launch per stage; the last 1x1 stage runs inside the decode kernel

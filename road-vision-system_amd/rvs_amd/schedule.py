@@ -20,7 +20,10 @@ Y2(j-1) || P(j+1) || Y1(j) || T(j-2) and joins all four before stage j+1.
 ``sync="flow"`` drops the joins and chains only the real dependencies with
 events: Y1(u) after P(u) and Y2(u-2) (its lane's workspace), Y2(u) after Y1(u)
 and T(u-4) (its candidate slot), P(u) after Y1(u-4) (its letterbox slot),
-T(u) after Y2(u).  Both give exactly the results of K sequential step()
+T(u) after Y2(u); and P(u+1) after Y1(u)'s forward part 3 (its stem and
+model.2, the VALU-bound start of the forward: the median pass of the next
+unit then overlaps the MFMA-bound rest of it).  Both give exactly the
+results of K sequential step()
 calls: every stream's frames reach SORT in order (all T stages run on one
 stream), and no buffer is rewritten before its reader finished.
 
@@ -253,6 +256,13 @@ class PipelinedRun:
         # competing for the process's hardware queues
         if os.environ.get("RV_TRACK_ON_Y2", "0") != "0":
             self.st = self.sm
+        # Y1(u) runs as forward parts 3 + 4 and the preprocess of unit u+1
+        # waits for part 3 (the VALU-bound stem and model.2 chain), so the
+        # VALU-bound median pass overlaps the MFMA-bound rest of the forward
+        # instead of the stem; Y1 is then issued before P (r04: +1.0 % with
+        # and without the consumer, five A/B pairs; RV_PREP_AFTER_STEM=0 is
+        # the r03 order)
+        self.prep_after_stem = os.environ.get("RV_PREP_AFTER_STEM", "1") != "0"
         self.sched = None
         self._events = None
         if mode == "native":
@@ -273,10 +283,16 @@ class PipelinedRun:
             k = self.k0[u] + h
             eng.preprocess_into(self.frames[k], self.procs[k], slot, h * S)
 
-    def _y1(self, u: int) -> None:
+    def _y1(self, u: int, E: "_Events" = None, stream=None) -> None:
         eng = self.eng
         S, slots = eng.S, eng.detector.slots
-        eng.yolo_stage(eng.detector.lb[u % slots][:self.units[u] * S], u % slots, u % 2, part=1)
+        lb = eng.detector.lb[u % slots][:self.units[u] * S]
+        if E is None:
+            eng.yolo_stage(lb, u % slots, u % 2, part=1)
+            return
+        eng.yolo_stage(lb, u % slots, u % 2, part=3)
+        E.record(("Y1a", u), stream)
+        eng.yolo_stage(lb, u % slots, u % 2, part=4)
 
     def _y2(self, u: int) -> None:
         slots = self.eng.detector.slots
@@ -311,13 +327,22 @@ class PipelinedRun:
                     E.wait(sm, ("T", u - slots))
                     self._y2(u)
                     E.record(("Y2", u), sm)
+            if self.prep_after_stem and 0 <= j < U:  # Y1(j) first, as parts 3 + 4
+                u = j
+                with torch.cuda.stream(sy):
+                    E.wait(sy, ("P", u))
+                    E.wait(sy, ("Y2", u - 2))
+                    self._y1(u, E, sy)
+                    E.record(("Y1", u), sy)
             if 0 <= j + 1 < U:  # P(j+1): after Y1(j+1-slots) read its letterbox slot
                 u = j + 1
                 with torch.cuda.stream(sp):
                     E.wait(sp, ("Y1", u - slots))
+                    if self.prep_after_stem:
+                        E.wait(sp, ("Y1a", u - 1))
                     self._prep(u)
                     E.record(("P", u), sp)
-            if 0 <= j < U:  # Y1(j): after P(j), and Y2(j-2) released lane j % 2
+            if not self.prep_after_stem and 0 <= j < U:  # Y1(j): after P(j), and Y2(j-2) released lane j % 2
                 u = j
                 with torch.cuda.stream(sy):
                     E.wait(sy, ("P", u))
