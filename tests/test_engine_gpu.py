@@ -111,23 +111,29 @@ def test_results_record_matches_device_outputs(cuda):
     eng.close()
 
 
-@pytest.mark.parametrize("mode,sync,pair,units", [
-    ("native", "flow", 1, None), ("native", "stage", 1, None), ("native", "flow", 2, None),
-    ("native", "stage", 2, None), ("eager", "flow", 2, None), ("eager", "stage", 1, None),
-    ("native", "flow", 4, [1, 2, 4, 1]), ("eager", "flow", 2, [1, 1, 2, 2, 1, 1])])
-def test_pipelined_run_matches_sequential_steps(cuda, mode, sync, pair, units):
+@pytest.mark.parametrize("mode,sync,pair,units,after_stem", [
+    ("native", "flow", 1, None, "1"), ("native", "stage", 1, None, "1"),
+    ("native", "flow", 2, None, "1"), ("native", "stage", 2, None, "1"),
+    ("eager", "flow", 2, None, "1"), ("eager", "stage", 1, None, "1"),
+    ("native", "flow", 4, [1, 2, 4, 1], "1"), ("eager", "flow", 2, [1, 1, 2, 2, 1, 1], "1"),
+    ("native", "flow", 2, None, "0"), ("eager", "flow", 4, [4, 2, 2], "0")])
+def test_pipelined_run_matches_sequential_steps(cuda, monkeypatch, mode, sync, pair, units,
+                                                after_stem):
     """bench.py's timed mode (rvs_amd.schedule.PipelinedRun): units of `pair`
     steps software-pipelined over four HIP streams -- preprocess of unit u+1,
     the two forward halves of units u and u-1 on two lanes, NMS + SORT +
     hand-back of unit u-2 -- issued by the native launch list or eagerly,
     lock-stepped or chained by per-dependency events; `units`: unequal unit
-    sizes (bench.py --units ramp: short units at both ends).  EVERY step's
+    sizes (bench.py --units ramp: short units at both ends); `after_stem`:
+    the next unit's preprocess waits for forward part 3 of the current one
+    (the default; "0" = one part 1, the r03 order).  EVERY step's
     handed-back detections / track ids and proc frames, and the final SORT
     state, must equal those of plain sequential step() calls; a second run()
     of the same schedule continues the tracks like K more step() calls."""
     from rvs_amd.engine import RoadVisionEngine
     from rvs_amd.schedule import PipelinedRun
     from rvs_amd.synth import road_frames
+    monkeypatch.setenv("RV_PREP_AFTER_STEM", after_stem)
     cfg = _cfg()
     S, H, W = 4, 1080, 1920
     K = 8  # a multiple of pair
@@ -223,9 +229,13 @@ def test_native_schedule_keeps_temporaries_and_checks_runs(cuda):
     run = PipelinedRun(eng, views, ts, mode="native")
     with pytest.raises(RVError):
         run.wait_step(0)  # no run yet
+    with pytest.raises(RVError):
+        run.step_ready(0)  # the non-blocking form, same rule
     torch.cuda.synchronize()
     churn = [torch.full((S, H, W, 3), 7, dtype=torch.uint8, device=cuda) for _ in range(4)]
     run.run()
+    while not run.step_ready(K - 1):
+        pass
     run.wait_step(K - 1)
     torch.cuda.synchronize()
     for k, o in enumerate(run.outs):
@@ -277,4 +287,24 @@ def test_bench_configuration_parity(cuda, pair):
     np.testing.assert_array_equal(st["T"], [len(t.tracks) for t in chk.trackers])
     assert chk.n_dets > 0
     run.close()
+    eng.close()
+
+
+def test_forward_part4_continues_part3(cuda):
+    """rv_yolo_forward_part part 4 (model.3 .. model.15) must continue the
+    handle's last part 3 (stem, model.2) with the same batch and workspace:
+    refused before any part 3 and for another batch."""
+    from rvs_amd._lib import RVError
+    from rvs_amd.engine import RoadVisionEngine
+    eng = RoadVisionEngine(_cfg(), 2, (720, 1280), device=cuda, lanes=2, pair=2)
+    det = eng.detector
+    lb = det.lb[0][:4]
+    with pytest.raises(RVError):
+        det.forward_raw(lb, lane=0, part=4)
+    det.forward_raw(lb, lane=0, part=3)
+    with pytest.raises(RVError):
+        det.forward_raw(det.lb[0][:2], lane=0, part=4)
+    det.forward_raw(lb, lane=0, part=4)
+    det.forward_raw(None, lane=0, part=2, batch=4)
+    torch.cuda.synchronize()
     eng.close()
