@@ -341,7 +341,13 @@ static bool epi_fast(const ConvArgs& a) {
 }
 
 // lane pixel opx (output pixel index b*Ho*Wo + y*Wo + x; valid = pv) of
-// each n; cout0 the block's first output channel
+// each n; cout0 the block's first output channel.  Fragments are stored in
+// pairs (m, m+1) as 16-B stores: lane quad q holds channels 4q .. 4q+3 of
+// both; one v_permlane16_swap per packed dword gives quad q the 8
+// consecutive channels 8 (q >> 1) .. +7 of fragment m + (q & 1) (the stem's
+// exchange), so a pair is one buffer_store_dwordx4 instead of two dwordx2 --
+// half the store instructions of the tile's epilogue.  Stores of invalid
+// pixels or of a fragment beyond Cout go to an out-of-range offset (dropped).
 template <int MR, int NR>
 __device__ __forceinline__ void epilogue_fast(const ConvArgs& a, f32x4 (&acc)[MR][NR], int cout0,
                                               const bool (&pv)[NR], const uint32_t (&opx)[NR],
@@ -350,31 +356,55 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& a, f32x4 (&acc)[MR
   const __amdgpu_buffer_rsrc_t rr =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.res, 0, 0x7FFFFFFF, kRsrcFlags);
   const int cq = cout0 + quad * 4;
+  constexpr uint32_t kDrop = 0x80000000u;
+  auto value = [&](int m, int n, uint32_t vr, uint32_t& lo, uint32_t& hi) {
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = acc[m][n][i] + bias[m][i];
+    if (a.act) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = silu(v[i]);
+    }
+    if (a.res) {
+      const uint2 q = __builtin_bit_cast(
+          uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(vr + m * 32), 0, 0));
+      v[0] += bf2f(q.x & 0xFFFF);
+      v[1] += bf2f(q.x >> 16);
+      v[2] += bf2f(q.y & 0xFFFF);
+      v[3] += bf2f(q.y >> 16);
+    }
+    lo = pack_bf16x2(v[0], v[1]);
+    hi = pack_bf16x2(v[2], v[3]);
+  };
 #pragma unroll
   for (int n = 0; n < NR; ++n) {
-    if (!pv[n]) continue;
+    if (!pv[n]) continue;  // all four quads of a pixel share pv: swap partners agree
     const uint32_t vo = (__umul24(opx[n], (uint32_t)a.out0_cs) + a.out0_co + cq) * 2;
     const uint32_t vr = a.res ? (__umul24(opx[n], (uint32_t)a.res_cs) + a.res_co + cq) * 2 : 0u;
+    // quad q's 16-B slot of pair (m, m+1): fragment m + (q & 1), channels
+    // 8 (q >> 1) .. +7, i.e. (16 (q & 1) + 8 (q >> 1) - 4 q) channels from
+    // its own dwordx2 slot
+    const uint32_t vo16 = vo + (16 * (quad & 1) + 8 * (quad >> 1) - 4 * quad) * 2;
 #pragma unroll
-    for (int m = 0; m < MR; ++m) {
+    for (int m = 0; m + 1 < MR; m += 2) {
       if (cout0 + m * 16 >= a.Cout) continue;  // block-uniform (Cout % 16 == 0)
-      float v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = acc[m][n][i] + bias[m][i];
-      if (a.act) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = silu(v[i]);
+      uint32_t a0, a1, b0, b1;
+      value(m, n, vr, a0, a1);
+      value(m + 1, n, vr, b0, b1);
+      const auto x0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+      const auto x1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+      const bool ok = cout0 + (m + (quad & 1)) * 16 < a.Cout;
+      const uint32_t off = ok ? vo16 + m * 32 : kDrop;
+      const v4u32 pk = {x0[0], x1[0], x0[1], x1[1]};
+      __builtin_amdgcn_raw_buffer_store_b128(pk, ro, (int)off, 0, 0);
+    }
+    if constexpr (MR & 1) {  // the last, unpaired fragment: one dwordx2 per lane
+      constexpr int m = MR - 1;
+      if (cout0 + m * 16 < a.Cout) {
+        uint32_t lo, hi;
+        value(m, n, vr, lo, hi);
+        __builtin_amdgcn_raw_buffer_store_b64(v2u32{lo, hi}, ro, (int)(vo + m * 32), 0, 0);
       }
-      if (a.res) {
-        const uint2 q = __builtin_bit_cast(
-            uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(vr + m * 32), 0, 0));
-        v[0] += bf2f(q.x & 0xFFFF);
-        v[1] += bf2f(q.x >> 16);
-        v[2] += bf2f(q.y & 0xFFFF);
-        v[3] += bf2f(q.y >> 16);
-      }
-      const uint2 pk = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, pk), ro, (int)(vo + m * 32), 0, 0);
     }
   }
 }

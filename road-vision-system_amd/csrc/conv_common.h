@@ -13,6 +13,7 @@ typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((ext_vector_type(2))) float f32x2v;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
 typedef __attribute__((ext_vector_type(2))) unsigned int v2u32;
+typedef __attribute__((ext_vector_type(4))) unsigned int v4u32;
 
 // f32 -> bf16, round to nearest even, on the hardware converter
 // (v_cvt_pk_bf16_f32: two values per instruction).
