@@ -234,6 +234,7 @@ __global__ __launch_bounds__(512) void c2f_chain_kernel(C2fArgs a) {
   constexpr int KC = (2 + N) * C;        // concat channels
   constexpr int NCH = (KC + 31) / 32;    // 32-channel k-steps
   constexpr int MR2 = 2 * C / 16;        // cv2 cout fragments (2C couts)
+  static_assert(MR2 % 2 == 0, "cv2 stores fragment pairs");
   constexpr int KP = NCH * 32;           // packed Cin (padded to 32)
   bf16x8c A2[NCH][MR2];
 #pragma unroll
@@ -285,12 +286,24 @@ __global__ __launch_bounds__(512) void c2f_chain_kernel(C2fArgs a) {
       const int gy = oy0 + r, gx = ox0 + c;
       if (gy >= a.H || gx >= a.W) continue;
       uint16_t* dst = a.out + ((size_t)(b * a.H + gy) * a.W + gx) * a.out_cs + a.out_co;
+      // fragment pairs (m, m+1) as 16-B stores: after one v_permlane16_swap
+      // per packed dword quad q holds channels 8 (q >> 1) .. +7 of fragment
+      // m + (q & 1) (conv.hip epilogue_fast); all quads of a pixel share
+      // the bounds test above
 #pragma unroll
-      for (int m = 0; m < MR2; ++m) {
-        float v[4];
+      for (int m = 0; m < MR2; m += 2) {
+        uint32_t pk[2][2];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = c2f_silu(acc[n][m][i] + bv2[m][i]);
-        *(uint2*)(dst + m * 16 + quad * 4) = make_uint2(c2f_pack(v[0], v[1]), c2f_pack(v[2], v[3]));
+        for (int h = 0; h < 2; ++h) {
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = c2f_silu(acc[n][m + h][i] + bv2[m + h][i]);
+          pk[h][0] = c2f_pack(v[0], v[1]);
+          pk[h][1] = c2f_pack(v[2], v[3]);
+        }
+        const auto x0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+        const auto x1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+        *(uint4*)(dst + (m + (quad & 1)) * 16 + (quad >> 1) * 8) = make_uint4(x0[0], x1[0], x0[1], x1[1]);
       }
     }
   }

@@ -399,11 +399,17 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
         d[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2[m], x1[n], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       if (oy >= H1 || ox >= W1) continue;
       uint16_t* o = out2 + (((size_t)b * H1 + oy) * W1 + ox) * out2_cs;
+      // the two fragments as one 16-B store per lane: after the swap quad q
+      // holds channels 8 (q >> 1) .. +7 of fragment q & 1 (as conv0 above)
+      uint32_t pk[2][2];
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
-        *(uint2*)(o + m * 16 + quad * 4) =
-            make_uint2(pack_bf16x2(silu(d[m][0] + bb2[m][0]), silu(d[m][1] + bb2[m][1])),
-                       pack_bf16x2(silu(d[m][2] + bb2[m][2]), silu(d[m][3] + bb2[m][3])));
+      for (int m = 0; m < 2; ++m) {
+        pk[m][0] = pack_bf16x2(silu(d[m][0] + bb2[m][0]), silu(d[m][1] + bb2[m][1]));
+        pk[m][1] = pack_bf16x2(silu(d[m][2] + bb2[m][2]), silu(d[m][3] + bb2[m][3]));
+      }
+      const auto y0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+      const auto y1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+      *(uint4*)(o + (quad & 1) * 16 + (quad >> 1) * 8) = make_uint4(y0[0], y1[0], y0[1], y1[1]);
     }
   }
 }
