@@ -173,6 +173,12 @@ int rv_yolo_destroy(void* handle);
  * model.2.cv1 from its registers) also writes the X1 map; by default X1
  * never reaches HBM when model.2.cv1 is fused. */
 #define RV_YOLO_OPT_STEM_X1 3
+/* RV_YOLO_OPT_HEAD_STREAMS (default 1): the P3 / P4 Detect heads run on two
+ * side streams of the handle (forked / joined with events) so they overlap
+ * the rest of the neck; 0 keeps them on the caller's stream (a pipelined
+ * caller whose stages already overlap).  The environment variable
+ * RV_HEAD_STREAMS=0/1 overrides it. */
+#define RV_YOLO_OPT_HEAD_STREAMS 4
 int rv_yolo_set_option(void* handle, int opt, int value);
 
 /* fp8 plans (BASELINE configs[4]: "YOLOv8m 1280x1280 fp8 MFMA conv path").

@@ -343,6 +343,7 @@ struct Model {
   int fuse_c2f = 1;
   // RV_YOLO_OPT_STEM_X1: the fused stem also writes X1 (parity tests)
   int stem_x1 = 0;
+  int head_streams = 1;            // RV_YOLO_OPT_HEAD_STREAMS
   std::vector<Buf> bufs;
   int nA = 0;
   int map_h[6], map_w[6];  // stride 2^i maps
@@ -945,6 +946,9 @@ extern "C" int rv_yolo_set_option(void* h, int opt, int value) {
     case RV_YOLO_OPT_STEM_X1:
       M->stem_x1 = value != 0;
       return RV_OK;
+    case RV_YOLO_OPT_HEAD_STREAMS:
+      M->head_streams = value != 0;
+      return RV_OK;
     default:
       set_error("unknown yolo option %d", opt);
       return RV_EINVAL;
@@ -1164,16 +1168,20 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
   // (RV_FUSE_HEAD=0: separate launches and f32 logits in HBM).  The P3 and
   // P4 heads are forked onto side streams as soon as their input map exists,
   // so they overlap the rest of the neck (small, latency-bound launches);
-  // RV_HEAD_STREAMS=0 keeps everything on the caller's stream.
+  // RV_YOLO_OPT_HEAD_STREAMS = 0 (a pipelined caller: its stages already
+  // overlap, and two more streams per handle share the process's 4 hardware
+  // queues -- r04: +3 % in the pipeline with the heads on the caller's
+  // stream) or RV_HEAD_STREAMS=0 / 1 (overrides) keeps everything on the
+  // caller's stream.
   const View P[3] = {View{M->X15, v.h15, 0}, View{M->X18, v.h18, 0}, View{M->X21, v.h21, 0}};
   const int dcs = v.c2d + v.c3d, hcs = 4 * v.reg + v.nc;
   static const bool fuse_env = !getenv("RV_FUSE_HEAD") || atoi(getenv("RV_FUSE_HEAD")) != 0;
   const bool fuse_head = fuse_env && v.c2d % 8 == 0 && v.c3d % 8 == 0;
-  static const bool streams_env =
-      !getenv("RV_HEAD_STREAMS") || atoi(getenv("RV_HEAD_STREAMS")) != 0;
+  static const int streams_env = getenv("RV_HEAD_STREAMS") ? atoi(getenv("RV_HEAD_STREAMS")) != 0 : -1;
+  const bool streams_on = streams_env >= 0 ? streams_env != 0 : M->head_streams != 0;
   // profiled forwards time every launch alone (per-launch roofline), so the
   // heads stay on the caller's stream there
-  const bool fork = streams_env && M->side[0] && M->side[1] &&
+  const bool fork = streams_on && M->side[0] && M->side[1] &&
                     !(M->prof.on && M->prof.n_fwd < M->prof.cap_fwd);
   const hipStream_t main_s = E.s;
   auto head_level = [&](int i) {

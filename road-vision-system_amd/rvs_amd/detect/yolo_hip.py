@@ -206,6 +206,12 @@ class YoloEngine:
         for h in self._hs:
             call("rv_yolo_set_option", h, 3, 1 if on else 0)
 
+    def set_head_streams(self, on: bool) -> None:
+        """The P3 / P4 Detect heads on the handle's two side streams (True,
+        default) or on the caller's stream (RV_YOLO_OPT_HEAD_STREAMS)."""
+        for h in self._hs:
+            call("rv_yolo_set_option", h, 4, 1 if on else 0)
+
     def set_fuse_c2f(self, on) -> None:
         """Narrow C2f blocks as one fused launch or one launch per conv
         (RV_YOLO_OPT_FUSE_C2F; bit-identical results): True / 1 = the

@@ -56,6 +56,12 @@ class RoadVisionEngine:
             max_det=int(det_cfg.get("max_det", 100)),
             classes_keep=[int(x) for x in det_cfg.get("classes_keep", [])], device=self.device,
             lanes=lanes)
+        if self.detector.lanes > 1:
+            # a multi-lane engine runs pipelined stages (schedule.PipelinedRun):
+            # its forwards keep the Detect heads on the stage's own stream
+            # instead of two more side streams per handle sharing the 4
+            # hardware queues (r04: +3 % frames/s; RV_HEAD_STREAMS overrides)
+            self.detector.set_head_streams(False)
         trk_cfg = cfg.get("tracking", {}) or {}
         self.tracker = MultiStreamSort(trk_cfg, self.S, tmax=tmax, dmax=self.detector.max_det,
                                        device=self.device)
