@@ -1040,6 +1040,33 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
   const bool fuse_c2f32 = fuse_c2f && (c2f32_env || M->fuse_c2f == 2);
   const int cat14 = v.h12 + v.c3, cat11 = v.c5 + v.c4, cat20 = v.h18 + v.c5,
             cat17 = v.h15 + v.h12;
+  // The neck's two Upsample + Concat pairs (yolov8.yaml layers 10-11 and
+  // 13-14): bf16 plans read the upsampled half of model.12.cv1's and
+  // model.15.cv1's input straight from the half-resolution map (a virtual
+  // concat, ConvArgs::split / in_up), so the 4x upsampled copies are never
+  // written; fp8 plans (patch kernel only) and RV_VCAT=0 materialise them
+  // into CAT11[0, c5) / CAT14[0, h12) as before.
+  static const bool vcat_env = !getenv("RV_VCAT") || atoi(getenv("RV_VCAT")) != 0;
+  const bool vcat = vcat_env && !f8;
+  const View none{-1, 0, 0};
+  const VIn vin12{View{M->CAT20, cat20, v.h18}, 1, View{M->CAT11, cat11, v.c5}, v.c5};
+  const VIn vin15{View{M->CAT17, cat17, v.h15}, 1, View{M->CAT14, cat14, v.h12}, v.h12};
+  auto c2f12 = [&]() {
+    E.c2f("model.12", View{M->CAT11, cat11, 0}, 4, M->C12, v.h12, v.nb, false,
+          View{M->CAT17, cat17, v.h15}, 0, vcat ? none : View{M->CAT14, cat14, 0}, vcat ? 0 : 1,
+          false, false, vcat ? &vin12 : nullptr);
+  };
+  auto c2f15 = [&]() {
+    E.c2f("model.15", View{M->CAT14, cat14, 0}, 3, M->C15, v.h15, v.nb, false,
+          View{M->X15, v.h15, 0}, 0, View{-1, 0, 0}, 0, v.h15 / 2 == 16 ? fuse_c2f : fuse_c2f32,
+          false, vcat ? &vin15 : nullptr);
+  };
+  // where part 1 ends (parts 1 / 4 vs part 2): after model.15 (15, default),
+  // model.12 (12) or SPPF (9) (RV_FWD_SPLIT).  Part 1 is the busier half
+  // (its stream 70 % busy against 45 % in the r04 trace), but moving the
+  // top-down neck's C2f blocks into part 2 measured slower (three A/B
+  // triples, r04: 44.6-45.1k at 15, 43.9-45.2k at 12, 43.6-44.7k at 9)
+  static const int split = getenv("RV_FWD_SPLIT") ? atoi(getenv("RV_FWD_SPLIT")) : 15;
   int st;
   if (part != 2) {
   if (part != 4) {  // part 4 continues after model.2
@@ -1137,32 +1164,21 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
   st = f8 ? launch_sppf_pool_fp8((uint8_t*)E.ptr(M->SP), B, M->map_h[5], M->map_w[5], sc, E.s)
           : launch_sppf_pool((bf16_t*)E.ptr(M->SP), B, M->map_h[5], M->map_w[5], sc, E.s);
   if (st) return st;
-  // The neck's two Upsample + Concat pairs (yolov8.yaml layers 10-11 and
-  // 13-14): bf16 plans read the upsampled half of model.12.cv1's and
-  // model.15.cv1's input straight from the half-resolution map (a virtual
-  // concat, ConvArgs::split / in_up), so the 4x upsampled copies are never
-  // written; fp8 plans (patch kernel only) and RV_VCAT=0 materialise them
-  // into CAT11[0, c5) / CAT14[0, h12) as before.
-  static const bool vcat_env = !getenv("RV_VCAT") || atoi(getenv("RV_VCAT")) != 0;
-  const bool vcat = vcat_env && !f8;
-  const View none{-1, 0, 0};
-  const VIn vin12{View{M->CAT20, cat20, v.h18}, 1, View{M->CAT11, cat11, v.c5}, v.c5};
-  const VIn vin15{View{M->CAT17, cat17, v.h15}, 1, View{M->CAT14, cat14, v.h12}, v.h12};
   E.conv("model.9.cv2", View{M->SP, 4 * sc, 0}, 5, View{M->CAT20, cat20, v.h18}, 0,
          vcat ? none : View{M->CAT11, cat11, 0}, vcat ? 0 : 1);
   // head
-  E.c2f("model.12", View{M->CAT11, cat11, 0}, 4, M->C12, v.h12, v.nb, false,
-        View{M->CAT17, cat17, v.h15}, 0, vcat ? none : View{M->CAT14, cat14, 0}, vcat ? 0 : 1,
-        false, false, vcat ? &vin12 : nullptr);
-  E.c2f("model.15", View{M->CAT14, cat14, 0}, 3, M->C15, v.h15, v.nb, false,
-        View{M->X15, v.h15, 0}, 0, View{-1, 0, 0}, 0, v.h15 / 2 == 16 ? fuse_c2f : fuse_c2f32,
-        false, vcat ? &vin15 : nullptr);
+  if (split >= 12) c2f12();
+  if (split >= 15) c2f15();
   if (E.status) return E.status;
   M->n_part1 = M->li_base + (int)M->launches.size();
   M->part1_B = B;
   M->part1_ws = ws;
   if (part == 1 || part == 4) return RV_OK;
   }  // part != 2
+  // the top-down neck's C2f blocks after the split run at the start of part 2
+  if (split < 12) c2f12();
+  if (split < 15) c2f15();
+  if (E.status) return E.status;
   // Detect head of level i: box (cv2) and class (cv3) branches, one grouped
   // launch per stage; the last 1x1 stage runs inside the decode kernel
   // (RV_FUSE_HEAD=0: separate launches and f32 logits in HBM).  The P3 and
