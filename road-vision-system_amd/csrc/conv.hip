@@ -1665,33 +1665,53 @@ __device__ __forceinline__ float head_sigmoid(float x) {
 // before the first MFMA, so the wave waits out one L2 latency instead of
 // one per (fragment, k-step) -- the runtime-bound loops compiled to a
 // load / s_waitcnt vmcnt(0) / MFMA chain.  Same k order and sums as the
-// generic loops (bit-identical logits).
+// generic loops (bit-identical logits).  The weight fragments (23 x 16 B
+// per lane) are loaded by head_weights once per level and stay in VGPRs
+// while the block walks its anchor tiles: per 16-anchor wave tile they were
+// 4.6x the feature bytes, all of it L2 -> CU traffic.
 template <int REG, int KB, int KC, int NCF>
-__device__ __forceinline__ void head_mfma_fixed(const HeadLevel& L, float* lg, int b, int HW, int r0,
-                                                int na, int nc) {
+__device__ __forceinline__ void head_weights(const HeadLevel& L, uint4 (&Ab)[KB][REG / 4],
+                                             uint4 (&Ac)[KC][NCF]) {
   constexpr int MB = REG / 4;
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
-  const int an0 = wave * 16 + col;
-  const bool ok = an0 < na;
-  const bf16_t* fp = L.feat + ((size_t)b * HW + r0 + (ok ? an0 : 0)) * L.feat_cs + quad * 8;
+  const int lane = threadIdx.x & 63, col = lane & 15, quad = lane >> 4;
   constexpr int cinb = KB * 32, cinc = KC * 32;
-  uint4 Bb[KB], Bc[KC], Ab[KB][MB], Ac[KC][NCF];
 #pragma unroll
-  for (int k = 0; k < KB; ++k) {
-    Bb[k] = ok && k * 32 + quad * 8 < L.cin_b ? *(const uint4*)(fp + k * 32) : make_uint4(0, 0, 0, 0);
+  for (int k = 0; k < KB; ++k)
 #pragma unroll
     for (int m = 0; m < MB; ++m)
       Ab[k][m] = *(const uint4*)(L.w_box + (size_t)(m * 16 + col) * cinb + k * 32 + quad * 8);
-  }
 #pragma unroll
-  for (int k = 0; k < KC; ++k) {
-    Bc[k] = ok && k * 32 + quad * 8 < L.cin_c ? *(const uint4*)(fp + 4 * REG + k * 32)
-                                              : make_uint4(0, 0, 0, 0);
+  for (int k = 0; k < KC; ++k)
 #pragma unroll
     for (int m = 0; m < NCF; ++m)
       Ac[k][m] = *(const uint4*)(L.w_cls + (size_t)(m * 16 + col) * cinc + k * 32 + quad * 8);
-  }
+}
+
+// one 16-anchor wave tile's feature fragments (B operands): box channels,
+// then class channels of anchor r0 + 16 wave + col
+template <int REG, int KB, int KC>
+__device__ __forceinline__ void head_feats(const HeadLevel& L, int b, int HW, int r0, int na,
+                                           uint4 (&Bb)[KB], uint4 (&Bc)[KC]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, quad = lane >> 4;
+  const int an0 = wave * 16 + col;
+  const bool ok = an0 < na;
+  const bf16_t* fp = L.feat + ((size_t)b * HW + r0 + (ok ? an0 : 0)) * L.feat_cs + quad * 8;
+#pragma unroll
+  for (int k = 0; k < KB; ++k)
+    Bb[k] = ok && k * 32 + quad * 8 < L.cin_b ? *(const uint4*)(fp + k * 32) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < KC; ++k)
+    Bc[k] = ok && k * 32 + quad * 8 < L.cin_c ? *(const uint4*)(fp + 4 * REG + k * 32)
+                                              : make_uint4(0, 0, 0, 0);
+}
+
+template <int REG, int KB, int KC, int NCF>
+__device__ __forceinline__ void head_mfma_fixed(const HeadLevel& L, const uint4 (&Ab)[KB][REG / 4],
+                                                const uint4 (&Ac)[KC][NCF], const uint4 (&Bb)[KB],
+                                                const uint4 (&Bc)[KC], float* lg, int nc) {
+  constexpr int MB = REG / 4;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
   float* row = lg + (size_t)(wave * 16 + col) * (L.cs + 4);
   {
     f32x4 acc[MB];
@@ -1739,234 +1759,256 @@ template <int REG, bool FUSED, int KB = 0, int KC = 0, int NCF = 0>
 __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B, int nc,
                                                             float conf, float* __restrict__ raw,
                                                             Cand* __restrict__ cand, int cap,
-                                                            int* __restrict__ seg_n) {
+                                                            int* __restrict__ seg_n, int nblk,
+                                                            int tpb) {
   extern __shared__ __attribute__((aligned(16))) float lg[];  // [64][cs + 4]
+  __shared__ int wcnt[4];
   const int b = blockIdx.y;
-  // block -> (level, first anchor in level).  Only compile-time indices
-  // into the by-value argument: a dynamic index would copy it to scratch.
-  const int blk = blockIdx.x;
-  int l = 0, A = h.start[1], lstart = 0, lblk = 0;
-  HeadLevel L = h.lv[0];
+  constexpr bool kFixed = FUSED && KC > 0;
+  uint4 Ab[kFixed ? KB : 1][REG / 4], Ac[kFixed ? KC : 1][kFixed ? NCF : 1];
+  uint4 Bb[kFixed ? KB : 1], Bc[kFixed ? KC : 1];  // the current tile's features
+  int wl = -1;       // level whose head weights are in Ab / Ac
+  bool pre = false;  // Bb / Bc already hold this tile's features
+  // The block walks anchor tiles blockIdx.x * tpb .. + tpb - 1 (64 anchors
+  // each; tpb > 1 only for the fixed fused head, whose weight fragments then
+  // stay in registers).  Every lg read of a tile precedes the block barrier
+  // before its candidate write-out, and a wave writes only its own 16 rows,
+  // so the next tile's MFMA section may overwrite the tile in place.
+  for (int t = 0; t < tpb; ++t) {
+    // block -> (level, first anchor in level).  Only compile-time indices
+    // into the by-value argument: a dynamic index would copy it to scratch.
+    const int blk = blockIdx.x * tpb + t;
+    if (blk >= nblk) break;  // block-uniform
+    int l = 0, A = h.start[1], lstart = 0, lblk = 0;
+    HeadLevel L = h.lv[0];
 #pragma unroll
-  for (int i = 1; i < 4; ++i) {
-    if (i < h.nlv) A = h.start[i + 1];
-    if (i < h.nlv && blk >= h.blk[i]) {
-      l = i;
-      L = h.lv[i];
-      lstart = h.start[i];
-      lblk = h.blk[i];
-    }
-  }
-  (void)l;
-  const int HW = L.H * L.W;
-  const int r0 = (blk - lblk) * 64;
-  const int na = min(64, HW - r0);
-  const int tid = threadIdx.x;
-  const int cs4 = L.cs / 4, ls4 = cs4 + 1;  // row length / LDS row stride in float4
-  if constexpr (FUSED && KC > 0) {
-    head_mfma_fixed<REG, KB, KC, NCF>(L, lg, b, HW, r0, na, nc);
-    __syncthreads();
-    if (L.logits_out) {  // parity/debug copy of the logits (coalesced rows)
-      f32x4* dst = (f32x4*)(L.logits_out + ((size_t)b * HW + r0) * L.cs);
-      for (int i = tid; i < na * cs4; i += 256) {
-        const int row = i / cs4, c4 = i - (i / cs4) * cs4;
-        dst[i] = ((const f32x4*)lg)[row * ls4 + c4];
+    for (int i = 1; i < 4; ++i) {
+      if (i < h.nlv) A = h.start[i + 1];
+      if (i < h.nlv && blk >= h.blk[i]) {
+        l = i;
+        L = h.lv[i];
+        lstart = h.start[i];
+        lblk = h.blk[i];
       }
     }
-  } else if constexpr (FUSED) {
-    constexpr int MB = REG / 4;  // box fragments (4*REG couts)
-    const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
-    const int an0 = wave * 16 + col;  // this lane's anchor (B column / D column)
-    const bool ok = an0 < na;
-    const bf16_t* fp = L.feat + ((size_t)b * HW + r0 + (ok ? an0 : 0)) * L.feat_cs + quad * 8;
-    const int ncf = (nc + 15) / 16;  // class fragments
-    float* lrow = lg + (size_t)an0 * (L.cs + 4);
-    // box: K = cin_b (multiple of 32)
-    {
-      f32x4 acc[MB];
-#pragma unroll
-      for (int m = 0; m < MB; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int cinp = (L.cin_b + 31) & ~31;
-      for (int k = 0; k < cinp; k += 32) {
-        const bool kv = ok && k + quad * 8 < L.cin_b;
-        const uint4 bv = kv ? *(const uint4*)(fp + k) : make_uint4(0, 0, 0, 0);
-        const bf16x8 Bf = __builtin_bit_cast(bf16x8, bv);
-#pragma unroll
-        for (int m = 0; m < MB; ++m) {
-          const bf16x8 Af = __builtin_bit_cast(
-              bf16x8, *(const uint4*)(L.w_box + (size_t)(m * 16 + col) * cinp + k + quad * 8));
-          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af, Bf, acc[m], 0, 0, 0);
+    const int HW = L.H * L.W;
+    const int r0 = (blk - lblk) * 64;
+    const int na = min(64, HW - r0);
+    const int tid = threadIdx.x;
+    const int cs4 = L.cs / 4, ls4 = cs4 + 1;  // row length / LDS row stride in float4
+    if constexpr (kFixed) {
+      if (l != wl) {
+        head_weights<REG, KB, KC, NCF>(L, Ab, Ac);
+        wl = l;
+      }
+      if (!pre) head_feats<REG, KB, KC>(L, b, HW, r0, na, Bb, Bc);
+      head_mfma_fixed<REG, KB, KC, NCF>(L, Ab, Ac, Bb, Bc, lg, nc);
+      // the next tile's features stream in under this tile's decode (same
+      // level only; a level change loads them at the top of its iteration)
+      pre = t + 1 < tpb && blk + 1 < nblk && r0 + 64 < HW;
+      if (pre) head_feats<REG, KB, KC>(L, b, HW, r0 + 64, min(64, HW - r0 - 64), Bb, Bc);
+      __syncthreads();
+      if (L.logits_out) {  // parity/debug copy of the logits (coalesced rows)
+        f32x4* dst = (f32x4*)(L.logits_out + ((size_t)b * HW + r0) * L.cs);
+        for (int i = tid; i < na * cs4; i += 256) {
+          const int row = i / cs4, c4 = i - (i / cs4) * cs4;
+          dst[i] = ((const f32x4*)lg)[row * ls4 + c4];
         }
       }
-      // lane holds couts m*16 + quad*4 + i of anchor `col` of this wave
+    } else if constexpr (FUSED) {
+      constexpr int MB = REG / 4;  // box fragments (4*REG couts)
+      const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
+      const int an0 = wave * 16 + col;  // this lane's anchor (B column / D column)
+      const bool ok = an0 < na;
+      const bf16_t* fp = L.feat + ((size_t)b * HW + r0 + (ok ? an0 : 0)) * L.feat_cs + quad * 8;
+      const int ncf = (nc + 15) / 16;  // class fragments
+      float* lrow = lg + (size_t)an0 * (L.cs + 4);
+      // box: K = cin_b (multiple of 32)
+      {
+        f32x4 acc[MB];
 #pragma unroll
-      for (int m = 0; m < MB; ++m) {
-        const int co = m * 16 + quad * 4;
-        const f32x4 bb = *(const f32x4*)(L.b_box + co);
-        *(f32x4*)(lg + (size_t)(wave * 16 + col) * (L.cs + 4) + co) = acc[m] + bb;
-      }
-    }
-    // classes: K = cin_c, couts nc (padded to 16)
-    {
-      const int cinp = (L.cin_c + 31) & ~31;
-      for (int m0 = 0; m0 < ncf; m0 += 5) {  // up to 5 fragments (80 classes) per pass
-        f32x4 acc[5];
-#pragma unroll
-        for (int m = 0; m < 5; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int m = 0; m < MB; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int cinp = (L.cin_b + 31) & ~31;
         for (int k = 0; k < cinp; k += 32) {
-          const bool kv = ok && k + quad * 8 < L.cin_c;
-          const uint4 bv = kv ? *(const uint4*)(fp + 4 * REG + k) : make_uint4(0, 0, 0, 0);
+          const bool kv = ok && k + quad * 8 < L.cin_b;
+          const uint4 bv = kv ? *(const uint4*)(fp + k) : make_uint4(0, 0, 0, 0);
           const bf16x8 Bf = __builtin_bit_cast(bf16x8, bv);
 #pragma unroll
-          for (int m = 0; m < 5; ++m) {
-            if (m0 + m >= ncf) break;
+          for (int m = 0; m < MB; ++m) {
             const bf16x8 Af = __builtin_bit_cast(
-                bf16x8,
-                *(const uint4*)(L.w_cls + (size_t)((m0 + m) * 16 + col) * cinp + k + quad * 8));
+                bf16x8, *(const uint4*)(L.w_box + (size_t)(m * 16 + col) * cinp + k + quad * 8));
             acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af, Bf, acc[m], 0, 0, 0);
           }
         }
+        // lane holds couts m*16 + quad*4 + i of anchor `col` of this wave
 #pragma unroll
-        for (int m = 0; m < 5; ++m) {
-          if (m0 + m >= ncf) break;
-          const int co = (m0 + m) * 16 + quad * 4;  // class index (bias padded to 16)
-          const f32x4 bb = *(const f32x4*)(L.b_cls + co);
-          float* d = lg + (size_t)(wave * 16 + col) * (L.cs + 4) + 4 * REG + co;
-          const f32x4 v = acc[m] + bb;
-          // the last fragment may run past nc: keep the padding out of the row
-          if (co + 3 < nc) {
-            *(f32x4*)d = v;
-          } else {
-            for (int i = 0; i < 4; ++i)
-              if (co + i < nc) d[i] = v[i];
+        for (int m = 0; m < MB; ++m) {
+          const int co = m * 16 + quad * 4;
+          const f32x4 bb = *(const f32x4*)(L.b_box + co);
+          *(f32x4*)(lg + (size_t)(wave * 16 + col) * (L.cs + 4) + co) = acc[m] + bb;
+        }
+      }
+      // classes: K = cin_c, couts nc (padded to 16)
+      {
+        const int cinp = (L.cin_c + 31) & ~31;
+        for (int m0 = 0; m0 < ncf; m0 += 5) {  // up to 5 fragments (80 classes) per pass
+          f32x4 acc[5];
+#pragma unroll
+          for (int m = 0; m < 5; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int k = 0; k < cinp; k += 32) {
+            const bool kv = ok && k + quad * 8 < L.cin_c;
+            const uint4 bv = kv ? *(const uint4*)(fp + 4 * REG + k) : make_uint4(0, 0, 0, 0);
+            const bf16x8 Bf = __builtin_bit_cast(bf16x8, bv);
+#pragma unroll
+            for (int m = 0; m < 5; ++m) {
+              if (m0 + m >= ncf) break;
+              const bf16x8 Af = __builtin_bit_cast(
+                  bf16x8,
+                  *(const uint4*)(L.w_cls + (size_t)((m0 + m) * 16 + col) * cinp + k + quad * 8));
+              acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af, Bf, acc[m], 0, 0, 0);
+            }
+          }
+#pragma unroll
+          for (int m = 0; m < 5; ++m) {
+            if (m0 + m >= ncf) break;
+            const int co = (m0 + m) * 16 + quad * 4;  // class index (bias padded to 16)
+            const f32x4 bb = *(const f32x4*)(L.b_cls + co);
+            float* d = lg + (size_t)(wave * 16 + col) * (L.cs + 4) + 4 * REG + co;
+            const f32x4 v = acc[m] + bb;
+            // the last fragment may run past nc: keep the padding out of the row
+            if (co + 3 < nc) {
+              *(f32x4*)d = v;
+            } else {
+              for (int i = 0; i < 4; ++i)
+                if (co + i < nc) d[i] = v[i];
+            }
           }
         }
       }
-    }
-    (void)lrow;
-    __syncthreads();
-    if (L.logits_out) {  // parity/debug copy of the logits (coalesced rows)
-      f32x4* dst = (f32x4*)(L.logits_out + ((size_t)b * HW + r0) * L.cs);
-      for (int i = tid; i < na * cs4; i += 256) {
-        const int row = i / cs4, c4 = i - (i / cs4) * cs4;
-        dst[i] = ((const f32x4*)lg)[row * ls4 + c4];
-      }
-    }
-  } else {
-    const f32x4* src = (const f32x4*)(L.logits + ((size_t)b * HW + r0) * L.cs);
-    // 8 loads in flight per thread before any LDS store (a plain copy loop
-    // would wait out one HBM latency per element)
-    for (int i0 = tid; i0 < na * cs4; i0 += 8 * 256) {
-      f32x4 v[8];  // native vectors (a float4 struct array would live in scratch)
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = i0 + u * 256;
-        v[u] = i < na * cs4 ? src[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = i0 + u * 256;
-        if (i < na * cs4) {
+      (void)lrow;
+      __syncthreads();
+      if (L.logits_out) {  // parity/debug copy of the logits (coalesced rows)
+        f32x4* dst = (f32x4*)(L.logits_out + ((size_t)b * HW + r0) * L.cs);
+        for (int i = tid; i < na * cs4; i += 256) {
           const int row = i / cs4, c4 = i - (i / cs4) * cs4;
-          ((f32x4*)lg)[row * ls4 + c4] = v[u];
+          dst[i] = ((const f32x4*)lg)[row * ls4 + c4];
         }
       }
+    } else {
+      const f32x4* src = (const f32x4*)(L.logits + ((size_t)b * HW + r0) * L.cs);
+      // 8 loads in flight per thread before any LDS store (a plain copy loop
+      // would wait out one HBM latency per element)
+      for (int i0 = tid; i0 < na * cs4; i0 += 8 * 256) {
+        f32x4 v[8];  // native vectors (a float4 struct array would live in scratch)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u * 256;
+          v[u] = i < na * cs4 ? src[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u * 256;
+          if (i < na * cs4) {
+            const int row = i / cs4, c4 = i - (i / cs4) * cs4;
+            ((f32x4*)lg)[row * ls4 + c4] = v[u];
+          }
+        }
+      }
+      __syncthreads();
     }
+    const int an = tid >> 2, part = tid & 3;
+    const bool live = an < na;
+    const float* px = lg + (live ? an : 0) * (L.cs + 4);
+    // DFL side `part`
+    float d;
+    {
+      float v[REG];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < REG; ++i) {
+        v[i] = px[part * REG + i];
+        mx = fmaxf(mx, v[i]);
+      }
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < REG; ++i) {
+        v[i] = __expf(v[i] - mx);
+        sum += v[i];
+      }
+      // softmax probabilities by one reciprocal (v_rcp_f32, <= 1 ulp from
+      // v / sum; the decode tolerance is 2e-3 px)
+      const float rs = __builtin_amdgcn_rcpf(sum);
+      float e = 0.f;
+#pragma unroll
+      for (int i = 0; i < REG; ++i) e += (float)i * (v[i] * rs);
+      d = e;
+    }
+    // classes part, part+4, ...: first maximum of the sigmoid scores
+    const float* pc = px + 4 * REG;
+    float best = -1.f;
+    int bc = 0;
+    for (int c = part; c < nc; c += 4) {
+      const float sg = head_sigmoid(pc[c]);
+      if (sg > best) {
+        best = sg;
+        bc = c;
+      }
+    }
+    // quad reduction: larger score, then smaller class index
+#pragma unroll
+    for (int off = 1; off < 4; off <<= 1) {
+      const float ob = __shfl_xor(best, off);
+      const int oc = __shfl_xor(bc, off);
+      if (ob > best || (ob == best && oc < bc)) {
+        best = ob;
+        bc = oc;
+      }
+    }
+    const int base = tid & ~3;
+    const float d0 = __shfl(d, base), d1 = __shfl(d, base + 1), d2 = __shfl(d, base + 2),
+                d3 = __shfl(d, base + 3);
+    const int r = r0 + (live ? an : 0);
+    const int a = lstart + r;
+    const int y = r / L.W, x = r - (r / L.W) * L.W;
+    const float ax = (float)x + 0.5f, ay = (float)y + 0.5f;
+    const float x1 = ax - d0, y1 = ay - d1, x2 = ax + d2, y2 = ay + d3;
+    const float cx = (x1 + x2) / 2.0f * L.stride, cy = (y1 + y2) / 2.0f * L.stride;
+    const float w = (x2 - x1) * L.stride, hh = (y2 - y1) * L.stride;
+    if (raw && live) {
+      for (int c = part; c < nc; c += 4)
+        raw[((size_t)b * (4 + nc) + 4 + c) * A + a] = head_sigmoid(pc[c]);
+      const float bxv = part == 0 ? cx : (part == 1 ? cy : (part == 2 ? w : hh));
+      raw[((size_t)b * (4 + nc) + part) * A + a] = bxv;
+    }
+    // Candidates go to this block's own 64-slot segment of the image's list
+    // (slot = segment * 64 + rank, ranks in anchor order) and the segment's
+    // count to seg_n: no cross-block atomics (same-address device atomics
+    // from thousands of waves serialise for ~100 us).
+    const bool pass = live && part == 0 && cand && best > conf;
+    const unsigned long long m = __ballot(pass);
+    const int wave = tid >> 6;
+    if ((tid & 63) == 0) wcnt[wave] = __popcll(m);
     __syncthreads();
-  }
-  const int an = tid >> 2, part = tid & 3;
-  const bool live = an < na;
-  const float* px = lg + (live ? an : 0) * (L.cs + 4);
-  // DFL side `part`
-  float d;
-  {
-    float v[REG];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < REG; ++i) {
-      v[i] = px[part * REG + i];
-      mx = fmaxf(mx, v[i]);
-    }
-    float sum = 0.f;
-#pragma unroll
-    for (int i = 0; i < REG; ++i) {
-      v[i] = __expf(v[i] - mx);
-      sum += v[i];
-    }
-    // softmax probabilities by one reciprocal (v_rcp_f32, <= 1 ulp from
-    // v / sum; the decode tolerance is 2e-3 px)
-    const float rs = __builtin_amdgcn_rcpf(sum);
-    float e = 0.f;
-#pragma unroll
-    for (int i = 0; i < REG; ++i) e += (float)i * (v[i] * rs);
-    d = e;
-  }
-  // classes part, part+4, ...: first maximum of the sigmoid scores
-  const float* pc = px + 4 * REG;
-  float best = -1.f;
-  int bc = 0;
-  for (int c = part; c < nc; c += 4) {
-    const float sg = head_sigmoid(pc[c]);
-    if (sg > best) {
-      best = sg;
-      bc = c;
-    }
-  }
-  // quad reduction: larger score, then smaller class index
-#pragma unroll
-  for (int off = 1; off < 4; off <<= 1) {
-    const float ob = __shfl_xor(best, off);
-    const int oc = __shfl_xor(bc, off);
-    if (ob > best || (ob == best && oc < bc)) {
-      best = ob;
-      bc = oc;
-    }
-  }
-  const int base = tid & ~3;
-  const float d0 = __shfl(d, base), d1 = __shfl(d, base + 1), d2 = __shfl(d, base + 2),
-              d3 = __shfl(d, base + 3);
-  const int r = r0 + (live ? an : 0);
-  const int a = lstart + r;
-  const int y = r / L.W, x = r - (r / L.W) * L.W;
-  const float ax = (float)x + 0.5f, ay = (float)y + 0.5f;
-  const float x1 = ax - d0, y1 = ay - d1, x2 = ax + d2, y2 = ay + d3;
-  const float cx = (x1 + x2) / 2.0f * L.stride, cy = (y1 + y2) / 2.0f * L.stride;
-  const float w = (x2 - x1) * L.stride, hh = (y2 - y1) * L.stride;
-  if (raw && live) {
-    for (int c = part; c < nc; c += 4)
-      raw[((size_t)b * (4 + nc) + 4 + c) * A + a] = head_sigmoid(pc[c]);
-    const float bxv = part == 0 ? cx : (part == 1 ? cy : (part == 2 ? w : hh));
-    raw[((size_t)b * (4 + nc) + part) * A + a] = bxv;
-  }
-  // Candidates go to this block's own 64-slot segment of the image's list
-  // (slot = segment * 64 + rank, ranks in anchor order) and the segment's
-  // count to seg_n: no cross-block atomics (same-address device atomics
-  // from thousands of waves serialise for ~100 us).
-  __shared__ int wcnt[4];
-  const bool pass = live && part == 0 && cand && best > conf;
-  const unsigned long long m = __ballot(pass);
-  const int wave = tid >> 6;
-  if ((tid & 63) == 0) wcnt[wave] = __popcll(m);
-  __syncthreads();
-  if (!cand) return;
-  int base0 = blk * 64;
-  for (int w2 = 0; w2 < wave; ++w2) base0 += wcnt[w2];
-  if (tid == 0) seg_n[(size_t)b * gridDim.x + blk] = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-  if (pass) {
-    const int i = base0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (i < cap) {
-      const float hw = w / 2.0f, hh2 = hh / 2.0f;  // xywh2xyxy
-      Cand c;
-      c.x1 = cx - hw;
-      c.y1 = cy - hh2;
-      c.x2 = cx + hw;
-      c.y2 = cy + hh2;
-      c.score = best;
-      c.cls = bc;
-      c.anchor = a;
-      c.pad = 0;
-      cand[(size_t)b * cap + i] = c;
+    if (!cand) continue;
+    int base0 = blk * 64;
+    for (int w2 = 0; w2 < wave; ++w2) base0 += wcnt[w2];
+    if (tid == 0) seg_n[(size_t)b * nblk + blk] = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    if (pass) {
+      const int i = base0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (i < cap) {
+        const float hw = w / 2.0f, hh2 = hh / 2.0f;  // xywh2xyxy
+        Cand c;
+        c.x1 = cx - hw;
+        c.y1 = cy - hh2;
+        c.x2 = cx + hw;
+        c.y2 = cy + hh2;
+        c.score = best;
+        c.cls = bc;
+        c.anchor = a;
+        c.pad = 0;
+        cand[(size_t)b * cap + i] = c;
+      }
     }
   }
 }
@@ -2013,7 +2055,8 @@ int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_ma
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();
   }
-  if (cand && cand_cap < h.blk[nlv] * 64) {
+  const int nblk = h.blk[nlv];
+  if (cand && cand_cap < nblk * 64) {
     set_error("detect decode: cand_cap %d < %d segments x 64", cand_cap, h.blk[nlv]);
     return RV_EINVAL;
   }
@@ -2023,15 +2066,20 @@ int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_ma
         set_error("fused head: bad level %d geometry", i);
         return RV_EINVAL;
       }
-    if (fixed)
-      detect_decode_kernel<16, true, 2, 3, 5><<<dim3(h.blk[nlv], B), 256, smem, s>>>(
-          h, B, nc, conf, raw, cand, cand_cap, cand_n);
-    else
-      detect_decode_kernel<16, true><<<dim3(h.blk[nlv], B), 256, smem, s>>>(h, B, nc, conf, raw, cand,
-                                                                            cand_cap, cand_n);
+    if (fixed) {
+      // anchor tiles per block: enough blocks to fill the chip several times
+      static const int tpb_env = getenv("RV_DECODE_TPB") ? atoi(getenv("RV_DECODE_TPB")) : 0;
+      int tpb = tpb_env > 0 ? tpb_env : 4;
+      while (tpb > 1 && (long)ceil_div(nblk, tpb) * B < 4L * num_cus()) --tpb;
+      detect_decode_kernel<16, true, 2, 3, 5><<<dim3(ceil_div(nblk, tpb), B), 256, smem, s>>>(
+          h, B, nc, conf, raw, cand, cand_cap, cand_n, nblk, tpb);
+    } else {
+      detect_decode_kernel<16, true><<<dim3(nblk, B), 256, smem, s>>>(h, B, nc, conf, raw, cand,
+                                                                      cand_cap, cand_n, nblk, 1);
+    }
   } else {
-    detect_decode_kernel<16, false><<<dim3(h.blk[nlv], B), 256, smem, s>>>(h, B, nc, conf, raw,
-                                                                           cand, cand_cap, cand_n);
+    detect_decode_kernel<16, false><<<dim3(nblk, B), 256, smem, s>>>(h, B, nc, conf, raw, cand,
+                                                                     cand_cap, cand_n, nblk, 1);
   }
   return launch_status("detect_decode");
 }
