@@ -1755,7 +1755,7 @@ __device__ __forceinline__ void head_mfma_fixed(const HeadLevel& L, const uint4 
   }
 }
 
-template <int REG, bool FUSED, int KB = 0, int KC = 0, int NCF = 0>
+template <int REG, bool FUSED, int KB = 0, int KC = 0, int NCF = 0, int NCT = 0>
 __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B, int nc,
                                                             float conf, float* __restrict__ raw,
                                                             Cand* __restrict__ cand, int cap,
@@ -1924,11 +1924,18 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
     {
       float v[REG];
       float mx = -INFINITY;
+      // the side's REG logits are 16-B aligned in the row (cs + 4 floats,
+      // a multiple of 4): ds_read_b128s
 #pragma unroll
-      for (int i = 0; i < REG; ++i) {
-        v[i] = px[part * REG + i];
-        mx = fmaxf(mx, v[i]);
+      for (int i = 0; i < REG; i += 4) {
+        const f32x4 q = *(const f32x4*)(px + part * REG + i);
+        v[i] = q[0];
+        v[i + 1] = q[1];
+        v[i + 2] = q[2];
+        v[i + 3] = q[3];
       }
+#pragma unroll
+      for (int i = 0; i < REG; ++i) mx = fmaxf(mx, v[i]);
       float sum = 0.f;
 #pragma unroll
       for (int i = 0; i < REG; ++i) {
@@ -1943,15 +1950,36 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
       for (int i = 0; i < REG; ++i) e += (float)i * (v[i] * rs);
       d = e;
     }
-    // classes part, part+4, ...: first maximum of the sigmoid scores
+    // first maximum of the sigmoid scores: classes part, part+4, ..., or
+    // (NCT: nc known at compile time, a multiple of 16) the contiguous
+    // quarter NCT/4 * part .. + NCT/4 - 1 as 16-B LDS reads.  Either way
+    // each lane keeps its first maximum and the quad reduction below picks
+    // the larger score, then the smaller class: the same (score, class).
     const float* pc = px + 4 * REG;
     float best = -1.f;
     int bc = 0;
-    for (int c = part; c < nc; c += 4) {
-      const float sg = head_sigmoid(pc[c]);
-      if (sg > best) {
-        best = sg;
-        bc = c;
+    if constexpr (NCT > 0) {
+      static_assert(NCT % 16 == 0, "contiguous class quarters of whole float4s");
+      constexpr int QC = NCT / 4;
+#pragma unroll
+      for (int j = 0; j < QC; j += 4) {
+        const f32x4 q = *(const f32x4*)(pc + part * QC + j);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float sg = head_sigmoid(q[i]);
+          if (sg > best) {
+            best = sg;
+            bc = part * QC + j + i;
+          }
+        }
+      }
+    } else {
+      for (int c = part; c < nc; c += 4) {
+        const float sg = head_sigmoid(pc[c]);
+        if (sg > best) {
+          best = sg;
+          bc = c;
+        }
       }
     }
     // quad reduction: larger score, then smaller class index
@@ -2071,7 +2099,7 @@ int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_ma
       static const int tpb_env = getenv("RV_DECODE_TPB") ? atoi(getenv("RV_DECODE_TPB")) : 0;
       int tpb = tpb_env > 0 ? tpb_env : 4;
       while (tpb > 1 && (long)ceil_div(nblk, tpb) * B < 4L * num_cus()) --tpb;
-      detect_decode_kernel<16, true, 2, 3, 5><<<dim3(ceil_div(nblk, tpb), B), 256, smem, s>>>(
+      detect_decode_kernel<16, true, 2, 3, 5, 80><<<dim3(ceil_div(nblk, tpb), B), 256, smem, s>>>(
           h, B, nc, conf, raw, cand, cand_cap, cand_n, nblk, tpb);
     } else {
       detect_decode_kernel<16, true><<<dim3(nblk, B), 256, smem, s>>>(h, B, nc, conf, raw, cand,
