@@ -1708,7 +1708,8 @@ __device__ __forceinline__ void head_feats(const HeadLevel& L, int b, int HW, in
 template <int REG, int KB, int KC, int NCF>
 __device__ __forceinline__ void head_mfma_fixed(const HeadLevel& L, const uint4 (&Ab)[KB][REG / 4],
                                                 const uint4 (&Ac)[KC][NCF], const uint4 (&Bb)[KB],
-                                                const uint4 (&Bc)[KC], float* lg, int nc) {
+                                                const uint4 (&Bc)[KC], float* lg, int nc,
+                                                float& best_out, int& bc_out) {
   constexpr int MB = REG / 4;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
@@ -1739,21 +1740,41 @@ __device__ __forceinline__ void head_mfma_fixed(const HeadLevel& L, const uint4 
       for (int m = 0; m < NCF; ++m)
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, Ac[k][m]),
                                                          __builtin_bit_cast(bf16x8, Bc[k]), acc[m], 0, 0, 0);
+    // the class scores never go to LDS: lane quad q holds classes
+    // m * 16 + 4 q + i of its anchor (ascending in (m, i)), so a scan keeps
+    // the lane's first maximum and two cross-quad steps (larger score, then
+    // smaller class) give the anchor's first maximum -- the (score, class)
+    // of a scan over all nc in order.  Same value per class as the LDS path
+    // (acc + bias, then head_sigmoid).
+    float best = -1.f;
+    int bc = 0;
 #pragma unroll
     for (int m = 0; m < NCF; ++m) {
       const int co = m * 16 + quad * 4;
       const f32x4 v = acc[m] + *(const f32x4*)(L.b_cls + co);
-      float* d = row + 4 * REG + co;
-      if (co + 3 < nc) {
-        *(f32x4*)d = v;
-      } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (co + i < nc) d[i] = v[i];
+      for (int i = 0; i < 4; ++i) {
+        const float sg = head_sigmoid(v[i]);
+        if (co + i < nc && sg > best) {
+          best = sg;
+          bc = co + i;
+        }
       }
     }
+#pragma unroll
+    for (int off = 16; off < 64; off <<= 1) {
+      const float ob = __shfl_xor(best, off);
+      const int oc = __shfl_xor(bc, off);
+      if (ob > best || (ob == best && oc < bc)) {
+        best = ob;
+        bc = oc;
+      }
+    }
+    best_out = best;
+    bc_out = bc;
   }
 }
+
 
 template <int REG, bool FUSED, int KB = 0, int KC = 0, int NCF = 0, int NCT = 0>
 __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B, int nc,
@@ -1769,6 +1790,8 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
   uint4 Bb[kFixed ? KB : 1], Bc[kFixed ? KC : 1];  // the current tile's features
   int wl = -1;       // level whose head weights are in Ab / Ac
   bool pre = false;  // Bb / Bc already hold this tile's features
+  float hbest = -1.f;  // fixed head: the lane's anchor's best class score / class
+  int hbc = 0;
   // The block walks anchor tiles blockIdx.x * tpb .. + tpb - 1 (64 anchors
   // each; tpb > 1 only for the fixed fused head, whose weight fragments then
   // stay in registers).  Every lg read of a tile precedes the block barrier
@@ -1802,19 +1825,12 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
         wl = l;
       }
       if (!pre) head_feats<REG, KB, KC>(L, b, HW, r0, na, Bb, Bc);
-      head_mfma_fixed<REG, KB, KC, NCF>(L, Ab, Ac, Bb, Bc, lg, nc);
+      head_mfma_fixed<REG, KB, KC, NCF>(L, Ab, Ac, Bb, Bc, lg, nc, hbest, hbc);
       // the next tile's features stream in under this tile's decode (same
       // level only; a level change loads them at the top of its iteration)
       pre = t + 1 < tpb && blk + 1 < nblk && r0 + 64 < HW;
       if (pre) head_feats<REG, KB, KC>(L, b, HW, r0 + 64, min(64, HW - r0 - 64), Bb, Bc);
       __syncthreads();
-      if (L.logits_out) {  // parity/debug copy of the logits (coalesced rows)
-        f32x4* dst = (f32x4*)(L.logits_out + ((size_t)b * HW + r0) * L.cs);
-        for (int i = tid; i < na * cs4; i += 256) {
-          const int row = i / cs4, c4 = i - (i / cs4) * cs4;
-          dst[i] = ((const f32x4*)lg)[row * ls4 + c4];
-        }
-      }
     } else if constexpr (FUSED) {
       constexpr int MB = REG / 4;  // box fragments (4*REG couts)
       const int wave = tid >> 6, lane = tid & 63, col = lane & 15, quad = lane >> 4;
@@ -1950,29 +1966,17 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
       for (int i = 0; i < REG; ++i) e += (float)i * (v[i] * rs);
       d = e;
     }
-    // first maximum of the sigmoid scores: classes part, part+4, ..., or
-    // (NCT: nc known at compile time, a multiple of 16) the contiguous
-    // quarter NCT/4 * part .. + NCT/4 - 1 as 16-B LDS reads.  Either way
-    // each lane keeps its first maximum and the quad reduction below picks
-    // the larger score, then the smaller class: the same (score, class).
+    // first maximum of the sigmoid scores.  The fixed head (NCT > 0) found
+    // it in registers (head_mfma_fixed: lane (col, quad) of the MFMA layout
+    // holds anchor col's result); otherwise lane part scans classes part,
+    // part + 4, ... in LDS and the quad reduction picks the larger score,
+    // then the smaller class.
     const float* pc = px + 4 * REG;
     float best = -1.f;
     int bc = 0;
     if constexpr (NCT > 0) {
-      static_assert(NCT % 16 == 0, "contiguous class quarters of whole float4s");
-      constexpr int QC = NCT / 4;
-#pragma unroll
-      for (int j = 0; j < QC; j += 4) {
-        const f32x4 q = *(const f32x4*)(pc + part * QC + j);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float sg = head_sigmoid(q[i]);
-          if (sg > best) {
-            best = sg;
-            bc = part * QC + j + i;
-          }
-        }
-      }
+      best = __shfl(hbest, (tid & 63) >> 2);
+      bc = __shfl(hbc, (tid & 63) >> 2);
     } else {
       for (int c = part; c < nc; c += 4) {
         const float sg = head_sigmoid(pc[c]);
@@ -1981,15 +1985,14 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
           bc = c;
         }
       }
-    }
-    // quad reduction: larger score, then smaller class index
 #pragma unroll
-    for (int off = 1; off < 4; off <<= 1) {
-      const float ob = __shfl_xor(best, off);
-      const int oc = __shfl_xor(bc, off);
-      if (ob > best || (ob == best && oc < bc)) {
-        best = ob;
-        bc = oc;
+      for (int off = 1; off < 4; off <<= 1) {
+        const float ob = __shfl_xor(best, off);
+        const int oc = __shfl_xor(bc, off);
+        if (ob > best || (ob == best && oc < bc)) {
+          best = ob;
+          bc = oc;
+        }
       }
     }
     const int base = tid & ~3;
@@ -2002,7 +2005,7 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
     const float x1 = ax - d0, y1 = ay - d1, x2 = ax + d2, y2 = ay + d3;
     const float cx = (x1 + x2) / 2.0f * L.stride, cy = (y1 + y2) / 2.0f * L.stride;
     const float w = (x2 - x1) * L.stride, hh = (y2 - y1) * L.stride;
-    if (raw && live) {
+    if (NCT == 0 && raw && live) {  // (the fixed head runs without raw / logits_out)
       for (int c = part; c < nc; c += 4)
         raw[((size_t)b * (4 + nc) + 4 + c) * A + a] = head_sigmoid(pc[c]);
       const float bxv = part == 0 ? cx : (part == 1 ? cy : (part == 2 ? w : hh));
@@ -2071,9 +2074,10 @@ int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_ma
   const bool fused = lv[0].feat != nullptr;
   // YOLOv8n's fused head (every level: box 64 -> 64, class 80 -> 80): the
   // compile-time MFMA section
-  bool fixed = fused && nc == 80;
+  // (it keeps the class scores in registers: no raw output, no logits copy)
+  bool fixed = fused && nc == 80 && raw == nullptr;
   for (int i = 0; i < nlv && fixed; ++i)
-    fixed = lv[i].cin_b == 64 && lv[i].cin_c == 80;
+    fixed = lv[i].cin_b == 64 && lv[i].cin_c == 80 && lv[i].logits_out == nullptr;
   static const bool fixed_env = !getenv("RV_DECODE_FIXED") || atoi(getenv("RV_DECODE_FIXED")) != 0;
   fixed = fixed && fixed_env;
   if (smem > 64 * 1024) {  // only raise the cap when the head needs it (large nc)

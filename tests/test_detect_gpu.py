@@ -177,6 +177,32 @@ def _iou(a, b):
     return inter / u if u > 0 else 0
 
 
+@pytest.mark.parametrize("H,W,B", [(1080, 1920, 4), (640, 640, 3)])
+def test_register_head_candidates_equal_lds_path(cuda, H, W, B):
+    """Without a raw output the YOLOv8n head decode keeps the class scores in
+    registers (detect_decode_kernel<..., NCT = 80>, blocks walking 4 anchor
+    tiles); with one it takes the LDS path that also writes raw.  Their
+    candidate segments are bit-identical: counts, boxes, scores, classes,
+    anchors and order."""
+    eng, _ = _engine(H, W, B, cuda)
+    lb = eng.letterbox(torch.from_numpy(_frames(H, W, B, seed=7)).to(cuda))
+    out = []
+    for with_raw in (False, True):
+        eng.cand[0].zero_()
+        eng.seg_n[0].zero_()
+        raw = torch.empty((B, 4 + eng.nc, eng.A), dtype=torch.float32,
+                          device=cuda) if with_raw else None
+        eng.forward_raw(lb, raw=raw)
+        torch.cuda.synchronize()
+        out.append((eng.seg_n[0, :B].cpu().numpy(), eng.cand[0, :B].cpu().numpy().view(np.int32)))
+    (n0, c0), (n1, c1) = out
+    assert np.array_equal(n0, n1) and n0.sum() > 0
+    for b in range(B):
+        for j in np.nonzero(n0[b])[0]:
+            k = int(n0[b, j])
+            assert np.array_equal(c0[b, 64 * j:64 * j + k], c1[b, 64 * j:64 * j + k]), (b, j)
+
+
 def _match_frac(a, b, min_score=0.27):
     """Fraction of the rows of `a` with score >= min_score matched by a row of
     `b` with the same class and IoU >= 0.9 (per image lists of (n, 6) rows).
