@@ -402,6 +402,17 @@ int rv_homography_project_f64(const double* H9, const float* boxes, int n,
                               const float* origin2, double max_distance,
                               double* out_xy, double* out_dist, void* stream);
 
+/* The tracker-off branch of the per-frame loop (main_preview.py:101-109:
+ * `tracker is None`): for dets (S x dmax x 6 f32, device) with det_n (S,
+ * device) valid rows per stream, out_id = -1 (track_id None), out_speed NaN
+ * (speed_kmh None) and out_dist = projector.distance_for_bbox(bbox)
+ * (projector.py:49-51; NaN = None) when H9 (host, 3x3 f64 row-major) is
+ * given, else NaN.  origin2 (host, 2 f32) is required with H9;
+ * max_distance < 0 = no cap.  Every out array is S x dmax, device. */
+int rv_untracked_metrics(const float* dets, const int* det_n, int S, int dmax,
+                         const double* H9, const float* origin2, double max_distance,
+                         int* out_id, double* out_dist, double* out_speed, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* Ingest: NV12 -> BGR (cv2.COLOR_YUV2BGR_NV12, 8U, BT.601 video range,      */
 /* 20-bit fixed point).  The device half of a decode front end for           */
@@ -521,7 +532,8 @@ int rv_capture_close(void* handle);
 #define RV_SCHED_NMS 4                    /* rv_nms_postprocess */
 #define RV_SCHED_SORT_UPDATE 5            /* rv_sort_update */
 #define RV_SCHED_HANDBACK 6               /* rv_results_handback */
-#define RV_SCHED_NUM_OPS 7
+#define RV_SCHED_UNTRACKED 7              /* rv_untracked_metrics */
+#define RV_SCHED_NUM_OPS 8
 int rv_sched_create(void** handle);
 int rv_sched_destroy(void* handle);
 int rv_sched_add_op(void* handle, int op, const int64_t* iargs, int ni, const double* fargs,
@@ -535,7 +547,11 @@ int rv_sched_num_nodes(void* handle);
 /* Host wait (this thread only) for record node `event` of the last run.
  * Valid only after rv_sched_run returned RV_OK for that run: RV_EINVAL
  * before the first run, while a run is issuing, after a run that failed
- * part-way, or for an event the latest run did not issue. */
+ * part-way, or for an event the latest run did not issue.  Single issuer:
+ * waits must not overlap an rv_sched_run of the same handle from another
+ * thread (issue a run, wait on its events, then issue the next run); the
+ * RV_EINVAL check covers a wait that starts while a run is issuing, not a
+ * run that starts while a wait polls. */
 int rv_sched_event_sync(void* handle, int event);
 /* Non-blocking form: 1 = completed, 0 = not yet, < 0 = error (same
  * validity rule as rv_sched_event_sync). */

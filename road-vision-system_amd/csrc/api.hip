@@ -17,7 +17,7 @@ void set_error(const char* fmt, ...) {
 }
 }  // namespace rv
 
-extern "C" int rv_abi_version(void) { return 5; }
+extern "C" int rv_abi_version(void) { return 6; }
 extern "C" const char* rv_last_error(void) { return rv::g_err; }
 
 // Trace marker: an empty one-wave kernel whose dispatch brackets a region of

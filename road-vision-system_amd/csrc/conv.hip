@@ -366,8 +366,11 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& a, f32x4 (&acc)[MR
       for (int i = 0; i < 4; ++i) v[i] = silu(v[i]);
     }
     if (a.res) {
+      // a fragment at or beyond Cout (the pair's second when Cout % 32 == 16)
+      // reads from an out-of-range offset: dropped, returns 0
+      const uint32_t roff = cout0 + m * 16 < a.Cout ? vr + m * 32 : kDrop;
       const uint2 q = __builtin_bit_cast(
-          uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(vr + m * 32), 0, 0));
+          uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)roff, 0, 0));
       v[0] += bf2f(q.x & 0xFFFF);
       v[1] += bf2f(q.x >> 16);
       v[2] += bf2f(q.y & 0xFFFF);

@@ -81,6 +81,7 @@ const OpSpec kSpecs[RV_SCHED_NUM_OPS] = {
     /* RV_SCHED_NMS */ {14, 2},
     /* RV_SCHED_SORT_UPDATE */ {16, 0},
     /* RV_SCHED_HANDBACK */ {10, 0},
+    /* RV_SCHED_UNTRACKED */ {9, 1},
 };
 
 int issue_op(const Node& n) {
@@ -129,6 +130,13 @@ int issue_op(const Node& n) {
       return rv_results_handback(P<const float>(a[0]), P<const int>(a[1]), P<const int>(a[2]),
                                  P<const double>(a[3]), P<const double>(a[4]), (int)a[5],
                                  (int)a[6], P<void>(a[7]), (size_t)a[8], P<void>(a[9]), s);
+    case RV_SCHED_UNTRACKED:
+      // dets, det_n, S, dmax, H9(host), origin2(host), [max_distance], out_id, out_dist,
+      // out_speed
+      return rv_untracked_metrics(P<const float>(a[0]), P<const int>(a[1]), (int)a[2], (int)a[3],
+                                  (const double*)host_arg(n, a[4]),
+                                  (const float*)host_arg(n, a[5]), f[0], P<int>(a[6]),
+                                  P<double>(a[7]), P<double>(a[8]), s);
   }
   set_error("rv_sched: unknown op %d", n.op);
   return RV_EINVAL;

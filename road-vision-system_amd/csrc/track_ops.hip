@@ -6,6 +6,8 @@
 //   rv_iou_matrix_batched     _iou_matrix   sort_tracker.py:74-80 (+ _iou :55-71)
 //   rv_greedy_assign_batched  _associate    sort_tracker.py:182-210 (the loop)
 //   rv_homography_project_f64 project_bbox + distance, projector.py:30-47,74-84
+//   rv_untracked_metrics      the tracker-off branch of main_preview.py:101-109:
+//                             no track ids or speeds, distance_for_bbox per det
 //
 // All latency-bound small work: one workgroup per stream for the IoU and
 // the assignment, one thread per box for the projection.
@@ -134,6 +136,39 @@ __global__ void project_kernel(const double* __restrict__ H, const float* __rest
   }
 }
 
+// The tracker-off branch of the reference loop (main_preview.py:101-109):
+// every detection keeps track_id / speed_kmh None and, with a projector,
+// gets distance_m = projector.distance_for_bbox(bbox) (None stays None).
+// One thread per (stream, detection) slot; slots past det_n[s] are written
+// as None too, so the hand-back record is well defined.
+struct UntrackedParams {
+  double H[9];
+  float origin[2];
+  double max_distance;
+  int has_proj;
+};
+
+__global__ void untracked_metrics_kernel(const float* __restrict__ dets,
+                                         const int* __restrict__ det_n, int S, int dmax,
+                                         UntrackedParams p, int* __restrict__ out_id,
+                                         double* __restrict__ out_dist,
+                                         double* __restrict__ out_speed) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S * dmax) return;
+  const int s = i / dmax, d = i - s * dmax;
+  double dist = NAN;
+  if (p.has_proj && d < min(max(det_n[s], 0), dmax)) {
+    const float* b = dets + 6 * (size_t)i;
+    const double cx = 0.5 * ((double)b[0] + (double)b[2]);
+    const double cy = (double)b[3];
+    double X, Y;
+    if (project_h(p.H, cx, cy, X, Y)) dist = distance_o(p.origin, p.max_distance, X, Y);
+  }
+  out_id[i] = -1;
+  out_dist[i] = dist;
+  out_speed[i] = NAN;
+}
+
 }  // namespace
 
 extern "C" int rv_iou_matrix_batched(const float* trk, const int* T, const float* det,
@@ -179,6 +214,31 @@ extern "C" int rv_homography_project_f64(const double* H9, const float* boxes, i
   project_kernel<<<ceil_div(n, 256), 256, 0, as_stream(stream)>>>(H9, boxes, n, origin2,
                                                                   max_distance, out_xy, out_dist);
   return launch_status("rv_homography_project_f64");
+}
+
+extern "C" int rv_untracked_metrics(const float* dets, const int* det_n, int S, int dmax,
+                                    const double* H9, const float* origin2, double max_distance,
+                                    int* out_id, double* out_dist, double* out_speed,
+                                    void* stream) {
+  RV_CHECK_ARG(dets != nullptr && det_n != nullptr && out_id != nullptr && out_dist != nullptr &&
+                   out_speed != nullptr,
+               "null pointer");
+  RV_CHECK_ARG(S >= 0 && dmax >= 1, "bad shape S=%d dmax=%d", S, dmax);
+  RV_CHECK_ARG(H9 == nullptr || origin2 != nullptr, "a projector needs its origin");
+  if (S == 0) return RV_OK;
+  UntrackedParams p{};
+  p.has_proj = H9 != nullptr;
+  if (H9)
+    for (int i = 0; i < 9; ++i) p.H[i] = H9[i];
+  if (origin2) {
+    p.origin[0] = origin2[0];
+    p.origin[1] = origin2[1];
+  }
+  p.max_distance = max_distance;
+  const int n = S * dmax;
+  untracked_metrics_kernel<<<ceil_div(n, 256), 256, 0, as_stream(stream)>>>(
+      dets, det_n, S, dmax, p, out_id, out_dist, out_speed);
+  return launch_status("rv_untracked_metrics");
 }
 
 }  // namespace rv

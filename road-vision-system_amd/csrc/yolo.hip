@@ -1146,6 +1146,11 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
     M->n_part1a = M->li_base + (int)M->launches.size();
     M->part1a_B = B;
     M->part1a_ws = ws;
+    // part 3 rewrote the start of the workspace: a part 2 now needs the part 4
+    // that finishes this forward, not the part 1 of an earlier one
+    M->n_part1 = -1;
+    M->part1_B = 0;
+    M->part1_ws = nullptr;
     return RV_OK;
   }
   }  // part != 4

@@ -60,6 +60,8 @@ _SIGS = {
                                          c_void_p, c_void_p]),
     "rv_homography_project_f64": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_double,
                                           c_void_p, c_void_p, c_void_p]),
+    "rv_untracked_metrics": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                     c_double, c_void_p, c_void_p, c_void_p, c_void_p]),
     # ingest
     "rv_nv12_to_bgr_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_size_t, c_size_t, c_void_p,
                                   c_int, c_int, c_int, c_int, c_void_p]),
@@ -194,7 +196,7 @@ def check(status: int, what: str = "") -> None:
 # stream-ordered calls a launch schedule can record (rvs_amd.schedule._OPS)
 _RECORDABLE = {"rv_clahe_median_letterbox_u8", "rv_clahe_median_u8", "rv_letterbox_u8",
                "rv_yolo_forward_part", "rv_nms_postprocess", "rv_sort_update",
-               "rv_results_handback"}
+               "rv_results_handback", "rv_untracked_metrics"}
 
 _NOCHECK = {"rv_sched_num_nodes", "rv_sched_event_query", "rv_abi_version", "rv_cand_segments", "rv_yolo_cand_segments", "rv_clahe_median_fits", "rv_clahe_median_letterbox_fits", "rv_yolo_num_convs", "rv_yolo_num_anchors",
             "rv_yolo_num_buffers", "rv_yolo_trace", "rv_yolo_profile_read", "rv_yolo_tuned_config",

@@ -46,38 +46,54 @@ class RoadVisionEngine:
         self.device = torch.device(device)
         self.pipeline = PreprocessPipeline(cfg.get("preprocess", {}) or {})
         det_cfg = cfg.get("detect", {}) or {}
-        self.variant = variant_of(det_cfg.get("model", "yolov8n.pt"))
-        if weights is None:
-            weights = weights_from_config(det_cfg, self.variant)
-        self.detector = YoloEngine(
-            self.variant, weights, self.S * self.pair, (self.H, self.W),
-            imgsz=int(det_cfg.get("imgsz", 640)),
-            conf=float(det_cfg.get("conf_thres", 0.25)), iou=float(det_cfg.get("iou_thres", 0.7)),
-            max_det=int(det_cfg.get("max_det", 100)),
-            classes_keep=[int(x) for x in det_cfg.get("classes_keep", [])], device=self.device,
-            lanes=lanes)
-        if self.detector.lanes > 1:
-            # a multi-lane engine runs pipelined stages (schedule.PipelinedRun):
-            # its forwards keep the Detect heads on the stage's own stream
-            # instead of two more side streams per handle sharing the 4
-            # hardware queues (r04: +3 % frames/s; RV_HEAD_STREAMS overrides)
-            self.detector.set_head_streams(False)
         trk_cfg = cfg.get("tracking", {}) or {}
-        self.tracker = MultiStreamSort(trk_cfg, self.S, tmax=tmax, dmax=self.detector.max_det,
-                                       device=self.device)
+        # main_preview.py:60-70: the detector and the tracker exist only when
+        # their `enabled` key is set (src/config.py defaults both to False)
+        self.detect_enabled = bool(det_cfg.get("enabled", False))
+        self.tracking_enabled = bool(trk_cfg.get("enabled", False))
+        self.variant = variant_of(det_cfg.get("model", "yolov8n.pt"))
+        self.detector = None
+        if self.detect_enabled:
+            if weights is None:
+                weights = weights_from_config(det_cfg, self.variant)
+            self.detector = YoloEngine(
+                self.variant, weights, self.S * self.pair, (self.H, self.W),
+                imgsz=int(det_cfg.get("imgsz", 640)),
+                conf=float(det_cfg.get("conf_thres", 0.25)),
+                iou=float(det_cfg.get("iou_thres", 0.7)),
+                max_det=int(det_cfg.get("max_det", 100)),
+                classes_keep=[int(x) for x in det_cfg.get("classes_keep", [])],
+                device=self.device, lanes=lanes)
+            if self.detector.lanes > 1:
+                # a multi-lane engine runs pipelined stages (schedule.PipelinedRun):
+                # its forwards keep the Detect heads on the stage's own stream
+                # instead of two more side streams per handle sharing the 4
+                # hardware queues (r04: +3 % frames/s; RV_HEAD_STREAMS overrides)
+                self.detector.set_head_streams(False)
+        self.max_det = self.detector.max_det if self.detector is not None else \
+            int(det_cfg.get("max_det", 100))
         if projector is None:
             geom = cfg.get("geometry", {}) or {}
             if geom.get("enabled", False):
                 projector = build_projector(geom)
         self.projector = projector
-        self.tracker.set_projector(projector)
+        self.tracker = None
+        if self.tracking_enabled and self.detector is not None:
+            self.tracker = MultiStreamSort(trk_cfg, self.S, tmax=tmax, dmax=self.max_det,
+                                           device=self.device)
+            self.tracker.set_projector(projector)
+        elif self.detector is not None:
+            # tracker off (main_preview.py:104-109): ids and speeds stay None,
+            # each detection gets projector.distance_for_bbox when a projector exists
+            self._untracked = _UntrackedMetrics(self.S, self.max_det, projector, self.device)
         self.proc = torch.empty((self.S, self.H, self.W, 3), dtype=torch.uint8, device=self.device)
         self.names = COCO80
         # result hand-back: device staging buffer + the pinned host record of step()
-        self.record = Record(self.S, self.detector.max_det, self.device)
+        self.record = Record(self.S, self.max_det, self.device)
         self.rec_stage = torch.empty(self.record.nbytes, dtype=torch.uint8, device=self.device)
         # default chain: CLAHE + median + the detector's LetterBox in one pass
-        self.fused_letterbox = self.pipeline.letterbox_fusable(self.H, self.W, self.detector.geo)
+        self.fused_letterbox = self.detector is not None and \
+            self.pipeline.letterbox_fusable(self.H, self.W, self.detector.geo)
 
     def preprocess_stage(self, frames: torch.Tensor, lb_slot: int = 0, lb_off: int = 0):
         """pipeline(raw) + the detector's LetterBox (main_preview.py:94-99)
@@ -88,6 +104,8 @@ class RoadVisionEngine:
             return self.pipeline.run_with_letterbox(frames, self.detector.geo,
                                                     self.detector.lb[lb_slot][lb_off:lb_off + B])
         proc = self.pipeline(frames)
+        if self.detector is None:
+            return proc, None
         return proc, self.detector.letterbox(proc, lb_slot, lb_off)
 
     def preprocess_into(self, frames: torch.Tensor, proc: torch.Tensor, lb_slot: int = 0,
@@ -133,7 +151,7 @@ class RoadVisionEngine:
         """NMS of candidate slot `slot` + SORT/geometry (main_preview.py:99-109),
         then the hand-back of the results into `record` (pinned host)."""
         dets, det_n = self.detector.nms(ts.shape[0], slot)
-        tid, dist, spd = self.tracker.update(dets, det_n, ts)
+        tid, dist, spd = self._metrics(dets, det_n, ts)
         out = {"dets": dets, "det_n": det_n, "track_id": tid, "distance_m": dist,
                "speed_kmh": spd}
         if record is not None:
@@ -152,7 +170,7 @@ class RoadVisionEngine:
         outs = []
         for h, (ts, rec) in enumerate(zip(ts_list, records)):
             d, n = dets[h * S:(h + 1) * S], det_n[h * S:(h + 1) * S]
-            tid, dist, spd = self.tracker.update(d, n, ts)
+            tid, dist, spd = self._metrics(d, n, ts)
             handback(d, n, tid, dist, spd, self.rec_stage, rec.host)
             outs.append({"record": rec})
         return outs
@@ -162,8 +180,16 @@ class RoadVisionEngine:
         """SORT + geometry of one step's NMS output (S images), then its
         hand-back into `record` (tracker.update + the .cpu() hand-over of
         main_preview.py:99-109)."""
-        tid, dist, spd = self.tracker.update(dets, det_n, ts)
+        tid, dist, spd = self._metrics(dets, det_n, ts)
         handback(dets, det_n, tid, dist, spd, self.rec_stage, record.host)
+
+    def _metrics(self, dets: torch.Tensor, det_n: torch.Tensor, ts: torch.Tensor):
+        """(track_id, distance_m, speed_kmh) of one step's NMS output:
+        SortTracker.update when tracking is enabled, else the tracker-off
+        branch of main_preview.py:101-109 (rv_untracked_metrics)."""
+        if self.tracker is not None:
+            return self.tracker.update(dets, det_n, ts)
+        return self._untracked(dets, det_n)
 
     def step_unit(self, frames_list, ts_list, records) -> List[Dict[str, torch.Tensor]]:
         """Pair mode, sequentially on the current stream: the preprocess of
@@ -183,7 +209,11 @@ class RoadVisionEngine:
         """frames (S,H,W,3) u8 on device, ts (S,) f64 on device.  The step's
         results end in `record` (pinned host; default: the engine's own
         record, which the next step() overwrites -- read results(out) before
-        it, or pass a Record per step)."""
+        it, or pass a Record per step).  With detect.enabled false only the
+        preprocess runs and every stream's list is empty (main_preview.py:97-99)."""
+        if self.detector is None:
+            proc, _ = self.preprocess_stage(frames)
+            return {"proc": proc, "no_detector": True}
         proc = self.detect_stage(frames, 0)
         out = self.track_stage(ts, 0, self.record if record is None else record)
         out["proc"] = proc
@@ -192,6 +222,8 @@ class RoadVisionEngine:
     def results(self, out: Dict[str, torch.Tensor]) -> List[List[Detection]]:
         """The reference's Detection lists of one step: from its host record
         (synchronises the device first), or from the device tensors."""
+        if out.get("no_detector"):
+            return [[] for _ in range(self.S)]
         if "record" in out:
             if "seq" in out and out["record"].seq != out["seq"]:
                 raise RuntimeError("this step's record was overwritten by a later step(): call "
@@ -219,8 +251,45 @@ class RoadVisionEngine:
         return res
 
     def track_stats(self) -> Dict[str, np.ndarray]:
-        """Per-stream SORT capacity report (MultiStreamSort.stats)."""
+        """Per-stream SORT capacity report (MultiStreamSort.stats); empty
+        arrays when tracking is off."""
+        if self.tracker is None:
+            z = np.zeros(self.S, np.int32)
+            return {"T": z, "next_id": z.copy(), "overflow": z.copy()}
         return self.tracker.stats()
 
     def close(self):
-        self.detector.close()
+        if self.detector is not None:
+            self.detector.close()
+
+
+class _UntrackedMetrics:
+    """The tracker-off outputs of one step (main_preview.py:101-109):
+    track_id None (-1), speed_kmh None (NaN), distance_m =
+    projector.distance_for_bbox(bbox) (projector.py:49-51) with a projector,
+    else None -- on the device (rv_untracked_metrics), so the step's
+    hand-back record is built exactly as with the tracker."""
+
+    def __init__(self, S: int, dmax: int, projector: Optional[GroundProjector], device):
+        self.S, self.dmax = int(S), int(dmax)
+        self.out_id = torch.empty((self.S, self.dmax), dtype=torch.int32, device=device)
+        self.out_dist = torch.empty((self.S, self.dmax), dtype=torch.float64, device=device)
+        self.out_speed = torch.empty((self.S, self.dmax), dtype=torch.float64, device=device)
+        self._H = self._origin = None
+        self._md = -1.0
+        if projector is not None:
+            H, origin, md = projector.device_params()
+            self._H = np.ascontiguousarray(H, np.float64)
+            self._origin = np.ascontiguousarray(origin, np.float32)
+            self._md = float(md)
+
+    def __call__(self, dets: torch.Tensor, det_n: torch.Tensor):
+        S = dets.shape[0]
+        if S != self.S or dets.shape[1] != self.dmax:
+            raise ValueError(f"dets must be ({self.S}, {self.dmax}, 6)")
+        _lib.call("rv_untracked_metrics", _lib.ptr(dets), _lib.ptr(det_n), S, self.dmax,
+                  self._H.ctypes.data if self._H is not None else None,
+                  self._origin.ctypes.data if self._origin is not None else None, self._md,
+                  _lib.ptr(self.out_id), _lib.ptr(self.out_dist), _lib.ptr(self.out_speed),
+                  _lib.stream_ptr())
+        return self.out_id, self.out_dist, self.out_speed

@@ -56,6 +56,14 @@ class Record:
                                      pool.items if pool is not None else None)
         return to_detections(*self.arrays(), names)
 
+    def arrays(self):
+        """(counts (S,), rows (S, dmax) structured) views of the host record.
+        The caller must have synchronised the stream that filled it."""
+        buf = self.host.numpy()
+        n = buf[:4 * self.S].view(np.int32)
+        rows = buf[_header(self.S):self.nbytes].view(ROW).reshape(self.S, self.dmax)
+        return n, rows
+
 
 class DetectionPool:
     """Pre-made Detection objects (every field None) for Record.detections:
@@ -73,14 +81,6 @@ class DetectionPool:
         k = int(n) - len(self.items)
         if k > 0 and _rvhandback is not None:
             self.items.extend(_rvhandback.shells(Detection, k))
-
-    def arrays(self):
-        """(counts (S,), rows (S, dmax) structured) views of the host record.
-        The caller must have synchronised the stream that filled it."""
-        buf = self.host.numpy()
-        n = buf[:4 * self.S].view(np.int32)
-        rows = buf[_header(self.S):self.nbytes].view(ROW).reshape(self.S, self.dmax)
-        return n, rows
 
 
 def handback(dets: torch.Tensor, det_n: torch.Tensor, track_id, distance_m, speed_kmh,

@@ -52,6 +52,7 @@ _OPS = {
     "rv_nms_postprocess": (4, 16, {}),
     "rv_sort_update": (5, 16, {8: 48, 9: 72, 10: 8}),
     "rv_results_handback": (6, 10, {}),
+    "rv_untracked_metrics": (7, 10, {4: 72, 5: 8}),
 }
 _FLOAT = (ctypes.c_float, ctypes.c_double)
 
@@ -217,6 +218,9 @@ class PipelinedRun:
             raise ValueError(f"mode {mode!r}: expected 'native' or 'eager'")
         if sync not in ("stage", "flow"):
             raise ValueError(f"sync {sync!r}: expected 'stage' or 'flow'")
+        if eng.detector is None:
+            raise ValueError("PipelinedRun needs detect.enabled (a detector-off engine runs "
+                             "only the preprocess: use step())")
         if eng.detector.lanes != 2:
             raise ValueError("PipelinedRun needs RoadVisionEngine(lanes=2)")
         P = eng.pair

@@ -306,5 +306,120 @@ def test_forward_part4_continues_part3(cuda):
         det.forward_raw(det.lb[0][:2], lane=0, part=4)
     det.forward_raw(lb, lane=0, part=4)
     det.forward_raw(None, lane=0, part=2, batch=4)
+    # a bare part 3 invalidates the earlier part 1 / 4: part 2 needs the part 4
+    # that continues it, never the stale model.3 .. model.15 activations
+    det.forward_raw(lb, lane=0, part=3)
+    with pytest.raises(RVError):
+        det.forward_raw(None, lane=0, part=2, batch=4)
+    det.forward_raw(lb, lane=0, part=4)
+    det.forward_raw(None, lane=0, part=2, batch=4)
     torch.cuda.synchronize()
+    eng.close()
+
+
+def _untracked_oracle(eng, cfg, proc, proj):
+    """Oracle detections of one step with the tracker off: the oracle NMS of
+    the GPU's own raw prediction, then main_preview.py:104-109 (distance_for_bbox
+    per detection when a projector exists; ids and speeds stay None)."""
+    raw = torch.empty((eng.S, 84, eng.detector.A), dtype=torch.float32, device=eng.device)
+    eng.detector.set_raw_fused(True)
+    eng.detector.forward_raw(eng.detector.letterbox(proc), raw, candidates=False)
+    eng.detector.set_raw_fused(False)
+    ref = yolo_ref.postprocess(raw.cpu().numpy(), (eng.detector.in_h, eng.detector.in_w),
+                               (eng.H, eng.W), classes_keep=cfg["detect"]["classes_keep"])
+    out = []
+    for s in range(eng.S):
+        lst = []
+        for r in ref[s]:
+            x1, y1, x2, y2, conf = map(float, r[:5])
+            dist = proj.distance_for_bbox((x1, y1, x2, y2)) if proj is not None else None
+            lst.append((x1, y1, x2, y2, conf, int(r[5]), None, dist, None))
+        out.append(lst)
+    return out
+
+
+@pytest.mark.parametrize("geometry", [True, False])
+def test_tracking_disabled_matches_oracle(cuda, geometry):
+    """tracking.enabled false (main_preview.py:64-70,101-109): no SORT runs;
+    every Detection keeps track_id / speed_kmh None and, with geometry on,
+    gets distance_m = projector.distance_for_bbox(bbox) -- compared field by
+    field with the oracle (boxes, conf, class exact; distances bit-exact)."""
+    from rvs_amd.engine import RoadVisionEngine
+    from rvs_amd.synth import road_frames
+    cfg = _cfg()
+    cfg["tracking"]["enabled"] = False
+    cfg["geometry"]["enabled"] = geometry
+    S, H, W, F = 3, 1080, 1920, 3
+    eng = RoadVisionEngine(cfg, S, (H, W), device=cuda)
+    assert eng.tracker is None
+    proj = sort_ref.HomographyProjector(eng.projector._H, (0.0, 0.0), 1000.0) if geometry else None
+    frames = road_frames(S, F, H, W, device=cuda)
+    n = 0
+    for f in range(F):
+        out = eng.step(frames[f], torch.full((S,), f / 30.0, dtype=torch.float64, device=cuda))
+        res = eng.results(out)
+        want = _untracked_oracle(eng, cfg, out["proc"], proj)
+        got = [[(d.x1, d.y1, d.x2, d.y2, d.conf, d.cls_id, d.track_id, d.distance_m, d.speed_kmh)
+                for d in s] for s in res]
+        # boxes / conf compared as the f32 values the reference's floats come from
+        for gs, ws in zip(got, want):
+            assert len(gs) == len(ws)
+            for g, w in zip(gs, ws):
+                assert np.float32(g[:5]).tobytes() == np.float32(w[:5]).tobytes()
+                assert g[5:] == w[5:]
+                assert g[6] is None and g[8] is None
+                assert (g[7] is None) == (not geometry)
+        n += sum(len(s) for s in res)
+    assert n > 0
+    eng.close()
+
+
+def test_tracking_disabled_pipelined_equals_steps(cuda):
+    """The pipelined native schedule with the tracker off (rv_untracked_metrics
+    recorded as a node) hands back exactly what sequential step() calls do."""
+    from rvs_amd.engine import RoadVisionEngine
+    from rvs_amd.schedule import PipelinedRun
+    from rvs_amd.synth import road_frames
+    cfg = _cfg()
+    cfg["tracking"]["enabled"] = False
+    S, H, W, K = 2, 1080, 1920, 4
+    frames = road_frames(S, K, H, W, device=cuda)
+    ts = [torch.full((S,), k / 30.0, dtype=torch.float64, device=cuda) for k in range(K)]
+    seq = RoadVisionEngine(cfg, S, (H, W), device=cuda)
+    key = lambda r: [[(d.x1, d.y1, d.x2, d.y2, d.conf, d.cls_id, d.track_id, d.distance_m,  # noqa
+                       d.speed_kmh) for d in s] for s in r]
+    want = [key(seq.results(seq.step(frames[k], ts[k]))) for k in range(K)]
+    pip = RoadVisionEngine(cfg, S, (H, W), device=cuda, lanes=2, pair=2)
+    run = PipelinedRun(pip, [frames[k] for k in range(K)], ts, mode="native")
+    run.run()
+    torch.cuda.synchronize()
+    for k, o in enumerate(run.outs):
+        assert key(pip.results(o)) == want[k]
+    assert any(d[7] is not None for r in want for s in r for d in s)
+    run.close()
+    seq.close()
+    pip.close()
+
+
+def test_detection_disabled_returns_empty_lists(cuda):
+    """detect.enabled false (main_preview.py:60-62,97-99): no detector is
+    built, the preprocess still produces proc (bit-exact), and every
+    stream's list is empty."""
+    from rvs_amd.engine import RoadVisionEngine
+    from rvs_amd.schedule import PipelinedRun
+    from rvs_amd.synth import road_frames
+    cfg = _cfg()
+    cfg["detect"]["enabled"] = False
+    S, H, W = 2, 720, 1280
+    eng = RoadVisionEngine(cfg, S, (H, W), device=cuda)
+    assert eng.detector is None and eng.tracker is None
+    frames = road_frames(S, 2, H, W, device=cuda)
+    out = eng.step(frames[0], torch.zeros(S, dtype=torch.float64, device=cuda))
+    assert eng.results(out) == [[], []]
+    src = frames[0].cpu().numpy()
+    pr = out["proc"].cpu().numpy()
+    for s in range(S):
+        np.testing.assert_array_equal(pr[s], cpu.median(cpu.clahe_ycrcb(src[s]), 3))
+    with pytest.raises(ValueError):
+        PipelinedRun(eng, [frames[0]], [torch.zeros(S, dtype=torch.float64, device=cuda)])
     eng.close()

@@ -128,3 +128,58 @@ def test_c_builder_pool_shells():
         assert all(x is y for x, y in zip(pool.items, spare))  # untouched shells stay
         ids = {id(o) for o in sum(got, [])}
         assert len(ids) == 50  # no object handed out twice
+
+
+def _cpu_record(n, rows):
+    """A Record over a plain CPU tensor (no pinned memory without a GPU)."""
+    import torch
+    from rvs_amd import handback
+    S, dmax = rows.shape
+    rec = object.__new__(handback.Record)
+    rec.S, rec.dmax = S, dmax
+    buf = _record_bytes(n, rows)
+    rec.nbytes = buf.size
+    rec.host = torch.from_numpy(buf)
+    rec.seq = 0
+    return rec
+
+
+def _random_rows(rng, S, dmax):
+    rows = np.zeros((S, dmax), ROW)
+    for f in ("x1", "y1", "x2", "y2", "conf"):
+        rows[f] = rng.uniform(-5, 2000, (S, dmax)).astype(np.float32)
+    rows["cls"] = rng.integers(-2, 84, (S, dmax))
+    rows["track_id"] = rng.integers(-1, 40, (S, dmax))
+    rows["dist"] = np.where(rng.random((S, dmax)) < 0.3, np.nan, rng.uniform(0, 9, (S, dmax)))
+    rows["speed"] = np.where(rng.random((S, dmax)) < 0.5, np.nan, rng.uniform(0, 9, (S, dmax)))
+    return rows
+
+
+def test_record_arrays_views_the_host_record():
+    """Record.arrays() is a Record method (not DetectionPool's) and returns
+    the count header and the 48-B rows of the host record."""
+    from rvs_amd import handback
+    assert hasattr(handback.Record, "arrays") and not hasattr(handback.DetectionPool, "arrays")
+    rng = np.random.default_rng(21)
+    rows = _random_rows(rng, 5, 7)
+    n = np.array([1, 0, 7, 3, 9], np.int32)
+    got_n, got_rows = _cpu_record(n, rows).arrays()
+    assert got_n.tolist() == n.tolist()
+    assert got_rows.tobytes() == rows.tobytes()
+
+
+def test_record_detections_without_c_builder(monkeypatch):
+    """With no C builder, Record.detections falls back to to_detections over
+    Record.arrays() and gives the same objects as the C path."""
+    from rvs_amd import handback
+    rng = np.random.default_rng(22)
+    rows = _random_rows(rng, 6, 11)
+    n = np.array([0, 4, 11, 2, -1, 15], np.int32)
+    rec = _cpu_record(n, rows)
+    want = to_detections(n, rows, COCO80)
+    c_built = rec.detections(COCO80) if handback._rvhandback is not None else want
+    monkeypatch.setattr(handback, "_rvhandback", None)
+    got = rec.detections(COCO80)
+    assert got == want == c_built
+    for a, b in zip(sum(got, []), sum(want, [])):
+        assert vars(a) == vars(b)
