@@ -698,10 +698,17 @@ def _cpu_baseline_leg(args, rank: int, world: int, cfg) -> dict:
     return {"cpu_baseline": cpu_baseline(cfg, args.cpu_frames, workers)}
 
 
-def _rank_fields(t: dict, world: int) -> dict:
-    return {"world_size": torch.distributed.get_world_size()
-            if torch.distributed.is_initialized() else 1,
+def _rank_fields(t: dict, world: int, device) -> dict:
+    """Per-rank fields of the line: the process group's size and backend,
+    every rank's own timed-region seconds and every rank's device identity
+    (PCI bus id; rvs_amd.shard.device_identity), both in rank order.  Every
+    rank must call this (the device ids are all-gathered)."""
+    from rvs_amd.shard import device_identity, gather_strings
+    init = torch.distributed.is_initialized()
+    return {"world_size": torch.distributed.get_world_size() if init else 1,
+            "process_group_backend": torch.distributed.get_backend() if init else None,
             "per_rank_local_s": [round(x, 6) for x in t["per_rank_s"]],
+            "per_rank_device": gather_strings(device_identity(device)),
             "local_s": round(t["local_s"], 6), "elapsed_s": round(t["elapsed_s"], 6)}
 
 
@@ -710,11 +717,12 @@ def _stub_main(args, rank, world) -> None:
     mod, cls = args.job.split(":")
     job = getattr(importlib.import_module(mod), cls)(args, rank, "cpu")
     t = rank_job(job, "cpu")
+    fields = _rank_fields(t, world, "cpu")
     if rank == 0:
         res = {"metric": METRIC, "value": t["value"], "unit": "frames/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": t["elapsed_s"] / args.steps * 1e3}
-        res.update(_rank_fields(t, world))
+        res.update(fields)
         res.update(_cpu_baseline_leg(args, rank, world, bench_config()))
         print(json.dumps(res), flush=True)
 
@@ -842,7 +850,7 @@ def main(argv=None):
         "sort": sort_rep,
         "handback": handback,
     }
-    res.update(_rank_fields(t, world))
+    res.update(_rank_fields(t, world, dev))
     if t2 is not None:
         res["device_only"] = {"value": round(t2["value"], 2),
                               "ms_per_step": round(t2["elapsed_s"] / K * 1e3, 4),

@@ -828,9 +828,43 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
         }
         continue;
       }
-      // kernel rows are not unrolled for the largest tiles: the fragments of
-      // one row (3 taps) in flight keep them under the register file
-#pragma unroll(F8 || MR * NR >= 16 ? 1 : K)
+      if constexpr (!F8) {
+        // bf16: the taps' fragment reads are software-pipelined one tap
+        // ahead -- tap t + 1's A / B fragments are read into the other
+        // register set before tap t's MFMAs issue, so the MFMAs of a tap
+        // never wait on the LDS reads issued right before them
+        bf16x8 Af[2][MR], Bq[2][NR];
+        auto ld = [&](int tap, int sl) {
+          const int ky = tap / K, kx = tap - (tap / K) * K;
+#pragma unroll
+          for (int m = 0; m < MR; ++m) {
+            const int row = m * 16 + col;
+            Af[sl][m] = __builtin_bit_cast(
+                bf16x8, *(const uint4*)(Wl + (row * T2 + tap) * 64 + ((quad ^ swzq<false>(row)) << 4)));
+          }
+#pragma unroll
+          for (int n = 0; n < NR; ++n)
+            Bq[sl][n] = __builtin_bit_cast(bf16x8, *(const uint4*)(P + ky * g.PW * PB + boff[n][kx]));
+        };
+        ld(0, 0);
+#pragma unroll
+        for (int t = 0; t < T2; ++t) {
+          // hard fences pin the order (the scheduler otherwise sinks each
+          // read next to its first use): tap t + 1's reads, then tap t's
+          // MFMAs, which wait only for the reads issued one tap earlier
+          if (t + 1 < T2) ld(t + 1, (t + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int m = 0; m < MR; ++m)
+#pragma unroll
+            for (int n = 0; n < NR; ++n)
+              acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[t & 1][m], Bq[t & 1][n],
+                                                                  acc[m][n], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        continue;
+      }
+#pragma unroll 1
       for (int ky = 0; ky < K; ++ky) {
         const uint8_t* Prow = P + ky * g.PW * PB;
 #pragma unroll

@@ -52,6 +52,35 @@ def gather_over_ranks(value: float, device=None) -> List[float]:
     return [float(x.item()) for x in out]
 
 
+def device_identity(device) -> str:
+    """Identity of this rank's device for the bench line: the GPU's PCI bus
+    id from hipDeviceGetPCIBusId (libamdhip64), so a multi-GPU line shows
+    that every rank ran on its own card; a CPU rank (gloo rehearsal) is
+    named host:pid."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return f"cpu:{os.uname().nodename}:{os.getpid()}"
+    import ctypes
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, int(idx)) == 0:
+            return buf.value.decode()
+    except OSError:
+        pass
+    return f"cuda:{idx}"
+
+
+def gather_strings(value: str) -> List[str]:
+    """Every rank's string, in rank order ([value] without a process group)."""
+    if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
+        return [str(value)]
+    out: List[Optional[str]] = [None] * torch.distributed.get_world_size()
+    torch.distributed.all_gather_object(out, str(value))
+    return [str(x) for x in out]
+
+
 def job_throughput(frames_per_rank: int, world: int, elapsed_max_s: float) -> float:
     """Whole-job frames/s: every rank's frames over the slowest rank's time."""
     return frames_per_rank * world / elapsed_max_s

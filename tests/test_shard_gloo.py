@@ -171,6 +171,10 @@ def test_bench_gpus_flag_spawns_the_ranks(tmp_path, capfd, monkeypatch):
     # every rank's own timed-region time, and the reported time is their max
     assert len(d["per_rank_local_s"]) == 2 and all(x > 0 for x in d["per_rank_local_s"])
     assert abs(max(d["per_rank_local_s"]) - d["elapsed_s"]) < 1e-5
+    # one device identity per rank, all distinct (on the GPU: PCI bus ids),
+    # and the process group's backend
+    assert len(d["per_rank_device"]) == 2 and len(set(d["per_rank_device"])) == 2
+    assert d["process_group_backend"] == "gloo" and d["world_size"] == 2
     # the CPU baseline rides in the N > 1 line too (rank 0, after the barrier)
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 0
