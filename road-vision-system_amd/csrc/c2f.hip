@@ -31,6 +31,7 @@
 // quarters (2, 3) of a B fragment read a zeroed LDS span instead of a
 // branch per tap.
 #include "conv.h"
+#include "conv_common.h"
 
 namespace rv {
 
@@ -43,9 +44,6 @@ __device__ __forceinline__ uint32_t c2f_pack(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2c{lo, hi}, bf16x2c));
 }
 __device__ __forceinline__ float c2f_bf2f(uint32_t h) { return __uint_as_float(h << 16); }
-__device__ __forceinline__ float c2f_silu(float v) {
-  return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
-}
 
 template <int C>
 struct C2fGeo {
@@ -142,7 +140,8 @@ __device__ __forceinline__ void c2f_conv3(const uint8_t* __restrict__ in, uint8_
       for (int m = 0; m < MR; ++m) {
         float v[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = c2f_silu(acc[n][m][i] + bv[m][i]);
+        for (int i = 0; i < 4; ++i) v[i] = acc[n][m][i] + bv[m][i];
+        silu4(v);
         const int lq = (m * 16 + quad * 4) >> 3, half = (quad & 1) * 8;
         if (RES) {
           const int d = e_res - e_out;
@@ -297,7 +296,8 @@ __global__ __launch_bounds__(512) void c2f_chain_kernel(C2fArgs a) {
         for (int h = 0; h < 2; ++h) {
           float v[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = c2f_silu(acc[n][m + h][i] + bv2[m + h][i]);
+          for (int i = 0; i < 4; ++i) v[i] = acc[n][m + h][i] + bv2[m + h][i];
+          silu4(v);
           pk[h][0] = c2f_pack(v[0], v[1]);
           pk[h][1] = c2f_pack(v[2], v[3]);
         }

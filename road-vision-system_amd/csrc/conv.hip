@@ -137,8 +137,7 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
       v[2] = acc[m][n][2] + bb.z;
       v[3] = acc[m][n][3] + bb.w;
       if (a.act) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = silu(v[i]);
+        silu4(v);
       }
       if (a.res) {
         const uint2 rr = *(const uint2*)(a.res + opix * a.res_cs + a.res_co + co);
@@ -362,8 +361,7 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& a, f32x4 (&acc)[MR
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = acc[m][n][i] + bias[m][i];
     if (a.act) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = silu(v[i]);
+      silu4(v);
     }
     if (a.res) {
       // a fragment at or beyond Cout (the pair's second when Cout % 32 == 16)
@@ -449,8 +447,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[MR][NR]
       v[2] = acc[m][n][2] + bias[m][2];
       v[3] = acc[m][n][3] + bias[m][3];
       if (a.act) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = silu(v[i]);
+        silu4(v);
       }
       if (a.res) {
         const uint2 rr = *(const uint2*)(a.res + opix * a.res_cs + a.res_co + co);
@@ -546,8 +543,7 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& a, f32x4 (&acc)[MR][NR
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = acc[m][n][i] * dq[m][i] + bias[m][i];
       if (a.act) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = silu(v[i]);
+        silu4(v);
       }
       if (a.res) {
         const uint32_t rr = *(const uint32_t*)((const uint8_t*)a.res + opix * a.res_cs + a.res_co + co);
@@ -619,7 +615,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
   constexpr int EB = F8 ? 1 : 2;              // bytes per element
   constexpr int CC = F8 ? 64 : 32;            // channels per chunk (64 B per pixel)
   const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
+  // the wave index as a scalar: every per-wave DMA test below is then a
+  // scalar branch, not an exec-mask region inside the MFMA stream
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int col = lane & 15, quad = lane >> 4;
   const int cout0 = blockIdx.y * BC;  // first output channel of the tile (output numbering)
   // the tile's group: its input slice, weights, bias and weight row base wc0
@@ -828,7 +826,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
         }
         continue;
       }
-      if constexpr (!F8) {
+      if constexpr (!F8 && MR * NR < 16) {
         // bf16: the taps' fragment reads are software-pipelined one tap
         // ahead -- tap t + 1's A / B fragments are read into the other
         // register set before tap t's MFMAs issue, so the MFMAs of a tap
@@ -864,7 +862,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
         }
         continue;
       }
-#pragma unroll 1
+      // (fp8, and the largest bf16 tiles, whose fragments of all taps in
+      // flight would exceed the register file: kernel rows not unrolled)
+#pragma unroll(F8 || MR * NR >= 16 ? 1 : K)
       for (int ky = 0; ky < K; ++ky) {
         const uint8_t* Prow = P + ky * g.PW * PB;
 #pragma unroll

@@ -28,6 +28,25 @@ __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint
 __device__ __forceinline__ float silu(float v) {
   return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
 }
+// The same SiLU on a pair: the scale by -log2(e) (what __expf(-v) lowers
+// to: one f32 multiply, then v_exp_f32), the + 1 and the final product run
+// as packed f32 pair instructions (v_pk_mul_f32 / v_pk_add_f32); element by
+// element these are the same IEEE operations as silu(), so the result is
+// bit-identical with half the non-transcendental instructions.
+__device__ __forceinline__ f32x2v silu2(f32x2v x) {
+  const float nl2e = __builtin_bit_cast(float, 0xBFB8AA3Bu);  // -log2(e) in f32
+  const f32x2v t = x * f32x2v{nl2e, nl2e};
+  const f32x2v d = f32x2v{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + 1.0f;
+  return x * f32x2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+// v[i] = SiLU(v[i]) for 4 values (two silu2 pairs)
+__device__ __forceinline__ void silu4(float (&v)[4]) {
+  const f32x2v a = silu2(f32x2v{v[0], v[1]}), b = silu2(f32x2v{v[2], v[3]});
+  v[0] = a.x;
+  v[1] = a.y;
+  v[2] = b.x;
+  v[3] = b.y;
+}
 
 // Buffer-resource LDS-DMA (conv_patch_kernel): dword3 of the descriptor
 // for a raw (stride 0) buffer on gfx950, and the voffset that the range

@@ -93,11 +93,15 @@ __device__ __forceinline__ void conv0_frag(const C0Wts<MR>& W, const i32x4 X, f3
     i32x4 t[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) t[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(W.d[m][i], X, W.c[m][i], 0, 0, 0);
+    float w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float u = fmaf((float)t[0][i], 65536.0f, (float)(t[1][i] * 256 + t[2][i]));
-      v[m][i] = silu(fmaf(W.s[m][i], u, W.b[m][i]));
+      w[i] = fmaf(W.s[m][i], u, W.b[m][i]);
     }
+    silu4(w);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[m][i] = w[i];
   }
 }
 
@@ -365,8 +369,11 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
     const f32x4 bb = *(const f32x4*)(b1 + 8 * quad + 4 * m);
 #pragma unroll
     for (int n = 0; n < NR; ++n) {
-      const uint32_t lo = pack_bf16x2(silu(acc[m][n][0] + bb[0]), silu(acc[m][n][1] + bb[1]));
-      const uint32_t hi = pack_bf16x2(silu(acc[m][n][2] + bb[2]), silu(acc[m][n][3] + bb[3]));
+      float w[4] = {acc[m][n][0] + bb[0], acc[m][n][1] + bb[1], acc[m][n][2] + bb[2],
+                    acc[m][n][3] + bb[3]};
+      silu4(w);
+      const uint32_t lo = pack_bf16x2(w[0], w[1]);
+      const uint32_t hi = pack_bf16x2(w[2], w[3]);
       x1[n][4 * m] = __builtin_bit_cast(__bf16, (uint16_t)(lo & 0xFFFF));
       x1[n][4 * m + 1] = __builtin_bit_cast(__bf16, (uint16_t)(lo >> 16));
       x1[n][4 * m + 2] = __builtin_bit_cast(__bf16, (uint16_t)(hi & 0xFFFF));
@@ -404,8 +411,11 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
       uint32_t pk[2][2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
-        pk[m][0] = pack_bf16x2(silu(d[m][0] + bb2[m][0]), silu(d[m][1] + bb2[m][1]));
-        pk[m][1] = pack_bf16x2(silu(d[m][2] + bb2[m][2]), silu(d[m][3] + bb2[m][3]));
+        float w[4] = {d[m][0] + bb2[m][0], d[m][1] + bb2[m][1], d[m][2] + bb2[m][2],
+                      d[m][3] + bb2[m][3]};
+        silu4(w);
+        pk[m][0] = pack_bf16x2(w[0], w[1]);
+        pk[m][1] = pack_bf16x2(w[2], w[3]);
       }
       const auto y0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
       const auto y1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
