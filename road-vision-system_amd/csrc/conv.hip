@@ -281,6 +281,15 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
 // Out-of-image pixels and channels >= Cin DMA from a zero block.
 // ---------------------------------------------------------------------------
 __device__ __attribute__((aligned(64))) uint4 g_zero16[4];
+#ifdef RV_PHASE_PROF
+// Timing build (-DRV_PHASE_PROF): s_memtime cycles per phase of
+// conv_patch_kernel summed over every wave of every launch: 0 prologue
+// (resident weights + first stage + barrier), 1 next-step DMA issue (incl.
+// the tile's offset prep), 2 compute, 3 epilogue, 4 end-of-step barrier
+// (incl. the vmcnt wait for the next stage), 5 steps, 6 waves.
+__device__ unsigned long long g_conv_phase[8];
+#define RV_PH_T() __builtin_amdgcn_s_memtime()
+#endif
 
 // XCD-aware pixel-tile walk.  Workgroups are dispatched to the 8 XCDs
 // round-robin by linear id, so with gridDim.x a multiple of 8 (the host
@@ -407,6 +416,100 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& a, f32x4 (&acc)[MR
         __builtin_amdgcn_raw_buffer_store_b64(v2u32{lo, hi}, ro, (int)(vo + m * 32), 0, 0);
       }
     }
+  }
+}
+
+// The patch kernel's form of epilogue_fast, split in two: epi_pack computes
+// the tile's packed bf16 outputs and their store offsets into registers
+// (the same values and store layout as epilogue_fast; invalid pixels and
+// fragments beyond Cout get the dropped offset, so every lane issues every
+// store), epi_store issues the stores.  The patch kernel packs before its
+// end-of-step barrier and stores after it, so the stores drain under the
+// next step's MFMAs instead of being waited for at that barrier
+// (s_waitcnt vmcnt(0) counts stores too: tools/conv_phase.py put 26 % of the
+// patch kernel's wave time in that wait).
+template <int MR, int NR>
+struct EpiPend {
+  v4u32 pk[MR / 2 > 0 ? MR / 2 : 1][NR];
+  uint32_t off[MR / 2 > 0 ? MR / 2 : 1][NR];
+  v2u32 pk1[NR];
+  uint32_t off1[NR];
+};
+
+template <int MR, int NR>
+__device__ __forceinline__ void epi_pack(const ConvArgs& a, f32x4 (&acc)[MR][NR], int cout0,
+                                         const bool (&pv)[NR], const uint32_t (&opx)[NR], int quad,
+                                         const f32x4 (&bias)[MR], EpiPend<MR, NR>& ep) {
+  const __amdgpu_buffer_rsrc_t rr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.res, 0, 0x7FFFFFFF, kRsrcFlags);
+  const int cq = cout0 + quad * 4;
+  constexpr uint32_t kDrop = 0x80000000u;
+  // residual: every fragment's 8-B load issued up front, one wait for all
+  // (a load then wait per fragment paid a full memory latency each, behind
+  // the next stage's DMA in the same in-order counter)
+  uint2 rq[MR][NR];
+  if (a.res) {
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      const uint32_t vr = (__umul24(opx[n], (uint32_t)a.res_cs) + a.res_co + cq) * 2;
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        const uint32_t roff = cout0 + m * 16 < a.Cout ? vr + m * 32 : kDrop;
+        rq[m][n] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)roff, 0, 0));
+      }
+    }
+  }
+  auto value = [&](int m, int n, uint32_t vr, uint32_t& lo, uint32_t& hi) {
+    (void)vr;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = acc[m][n][i] + bias[m][i];
+    if (a.act) silu4(v);
+    if (a.res) {
+      const uint2 q = rq[m][n];
+      v[0] += bf2f(q.x & 0xFFFF);
+      v[1] += bf2f(q.x >> 16);
+      v[2] += bf2f(q.y & 0xFFFF);
+      v[3] += bf2f(q.y >> 16);
+    }
+    lo = pack_bf16x2(v[0], v[1]);
+    hi = pack_bf16x2(v[2], v[3]);
+  };
+#pragma unroll
+  for (int n = 0; n < NR; ++n) {
+    const uint32_t vo = (__umul24(opx[n], (uint32_t)a.out0_cs) + a.out0_co + cq) * 2;
+    const uint32_t vr = a.res ? (__umul24(opx[n], (uint32_t)a.res_cs) + a.res_co + cq) * 2 : 0u;
+    const uint32_t vo16 = vo + (16 * (quad & 1) + 8 * (quad >> 1) - 4 * quad) * 2;
+#pragma unroll
+    for (int m = 0; m + 1 < MR; m += 2) {
+      uint32_t a0, a1, b0, b1;
+      value(m, n, vr, a0, a1);
+      value(m + 1, n, vr, b0, b1);
+      const auto x0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+      const auto x1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+      const bool ok = pv[n] && cout0 + (m + (quad & 1)) * 16 < a.Cout;
+      ep.off[m / 2][n] = ok ? vo16 + m * 32 : kDrop;
+      ep.pk[m / 2][n] = v4u32{x0[0], x1[0], x0[1], x1[1]};
+    }
+    if constexpr (MR & 1) {
+      constexpr int m = MR - 1;
+      uint32_t lo, hi;
+      value(m, n, vr, lo, hi);
+      ep.off1[n] = pv[n] && cout0 + m * 16 < a.Cout ? vo + m * 32 : kDrop;
+      ep.pk1[n] = v2u32{lo, hi};
+    }
+  }
+}
+
+template <int MR, int NR>
+__device__ __forceinline__ void epi_store(const ConvArgs& a, const EpiPend<MR, NR>& ep) {
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(a.out0, 0, 0x7FFFFFFF, kRsrcFlags);
+#pragma unroll
+  for (int n = 0; n < NR; ++n) {
+#pragma unroll
+    for (int m = 0; m + 1 < MR; m += 2)
+      __builtin_amdgcn_raw_buffer_store_b128(ep.pk[m / 2][n], ro, (int)ep.off[m / 2][n], 0, 0);
+    if constexpr (MR & 1) __builtin_amdgcn_raw_buffer_store_b64(ep.pk1[n], ro, (int)ep.off1[n], 0, 0);
   }
 }
 
@@ -912,6 +1015,17 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
   };
 
   if (nsteps == 0) return;
+#ifdef RV_PHASE_PROF
+  unsigned long long ph[5] = {0, 0, 0, 0, 0}, t_ph = RV_PH_T();
+#define RV_PH(i)                             \
+  {                                          \
+    const unsigned long long t_ = RV_PH_T(); \
+    ph[i] += t_ - t_ph;                      \
+    t_ph = t_;                               \
+  }
+#else
+#define RV_PH(i)
+#endif
   int ti = walk.t0;  // tile of the current step
   int grp = 0;       // chunk group of the current step
   if constexpr (RESW)
@@ -919,6 +1033,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
   prep_tile(ti);
   stage(0, 0);
   __syncthreads();
+  RV_PH(0);
   for (int s = 0; s < nsteps; ++s) {
     if (grp == 0) {
 #pragma unroll
@@ -932,7 +1047,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
       if (last) prep_tile(ti + walk.step);
       stage(last ? 0 : grp + 1, (s + 1) & 1);
     }
+    RV_PH(1);
     compute(grp, s & 1);
+    RV_PH(2);
+    // a finished tile's packed outputs, stored after the barrier (tiles whose
+    // pack registers fit beside the compute registers without spills)
+    constexpr bool kDefer = !F8 && MR * NR < 10;
+    EpiPend<MR, NR> ep;
     if (last) {
       const int b = ti / tiles_img;
       const int r = ti - b * tiles_img;
@@ -964,17 +1085,34 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
         uint32_t opx[NR];
 #pragma unroll
         for (int n = 0; n < NR; ++n) opx[n] = (uint32_t)((b * a.Ho + py[n]) * a.Wo + px[n]);
-        epilogue_fast<MR, NR>(a, acc, cout0, pv, opx, quad, bias);
+        if constexpr (kDefer)
+          epi_pack<MR, NR>(a, acc, cout0, pv, opx, quad, bias, ep);
+        else
+          epilogue_fast<MR, NR>(a, acc, cout0, pv, opx, quad, bias);
       } else {
         epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias);
       }
       ti += walk.step;
       grp = 0;
+      RV_PH(3);
     } else {
       ++grp;
     }
     __syncthreads();
+    if constexpr (kDefer) {
+      if (last && g.fast) epi_store<MR, NR>(a, ep);  // the finished tile's stores (epi_pack)
+    }
+    RV_PH(4);
   }
+#ifdef RV_PHASE_PROF
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_conv_phase[i], ph[i]);
+    atomicAdd(&g_conv_phase[5], (unsigned long long)nsteps);
+    atomicAdd(&g_conv_phase[6], 1ull);
+  }
+#endif
+#undef RV_PH
 }
 
 
@@ -1378,6 +1516,21 @@ bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c) {
   return patch_geo(a, c, g, sm);
 }
 
+#ifdef RV_PHASE_PROF
+}  // namespace rv
+// Timing build only (not in include/rvhip.h): read (and with reset != 0
+// clear) the conv_patch_kernel phase sums, 8 x u64.
+extern "C" int rv_conv_phase_read(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rv::g_conv_phase), 8 * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  if (reset) {
+    static const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rv::g_conv_phase), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+namespace rv {
+#endif
 int launch_conv_cfg(const ConvArgs& a, const ConvCfg& c, hipStream_t s) {
   PatchGeo g;
   size_t sm;
