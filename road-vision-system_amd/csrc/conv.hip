@@ -794,16 +794,27 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
       aoff[m][1] = base + (((2 * (quad & 1) + 1) ^ sw) << 4);
     }
   }
-  f32x4 bias[MR], dq[MR];
+  // bf16: the block's bias lives in LDS (BC floats after the two stages;
+  // patch_geo sizes it) and is read back per tile in the epilogue, so its
+  // 4 * MR registers are free during the MFMA loop.  fp8 keeps bias and
+  // dequantisation scales in registers.
+  float* const bias_lds = (float*)(stages + 2 * stage_bytes);
+  f32x4 bias[F8 ? MR : 1], dq[F8 ? MR : 1];
+  if constexpr (F8) {
 #pragma unroll
-  for (int m = 0; m < MR; ++m) {
-    const int co = wc0 + m * 16 + quad * 4;  // bias is padded to Cout_pad16
-    bias[m] = co < wcout_pad ? *(const f32x4*)(bias_p + co) : f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (F8) {
+    for (int m = 0; m < MR; ++m) {
+      const int co = wc0 + m * 16 + quad * 4;  // bias is padded to Cout_pad16
+      bias[m] = co < wcout_pad ? *(const f32x4*)(bias_p + co) : f32x4{0.f, 0.f, 0.f, 0.f};
       const f32x4 ws = co < wcout_pad ? *(const f32x4*)(wsc_p + co) : f32x4{0.f, 0.f, 0.f, 0.f};
       dq[m] = ws * a.s_in;
     }
+  } else {
+    for (int i = tid; i < BC; i += 64 * NW) bias_lds[i] = wc0 + i < wcout_pad ? bias_p[wc0 + i] : 0.f;
   }
+  auto bias_tile = [&](f32x4 (&bl)[MR]) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m) bl[m] = *(const f32x4*)(bias_lds + m * 16 + quad * 4);
+  };
   // Patch and weight DMA through buffer resources (buffer_load ... lds):
   // every DMA instruction's per-lane byte offset is computed once -- per
   // tile for the patch, per kernel for the weights --, the chunk offset
@@ -1052,7 +1063,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
     RV_PH(2);
     // a finished tile's packed outputs, stored after the barrier (tiles whose
     // pack registers fit beside the compute registers without spills)
-    constexpr bool kDefer = !F8 && MR * NR < 10;
+    constexpr bool kDefer = !F8 && MR * NR <= 10;
     EpiPend<MR, NR> ep;
     if (last) {
       const int b = ti / tiles_img;
@@ -1085,12 +1096,16 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
         uint32_t opx[NR];
 #pragma unroll
         for (int n = 0; n < NR; ++n) opx[n] = (uint32_t)((b * a.Ho + py[n]) * a.Wo + px[n]);
+        f32x4 bl[MR];
+        bias_tile(bl);
         if constexpr (kDefer)
-          epi_pack<MR, NR>(a, acc, cout0, pv, opx, quad, bias, ep);
+          epi_pack<MR, NR>(a, acc, cout0, pv, opx, quad, bl, ep);
         else
-          epilogue_fast<MR, NR>(a, acc, cout0, pv, opx, quad, bias);
+          epilogue_fast<MR, NR>(a, acc, cout0, pv, opx, quad, bl);
       } else {
-        epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias);
+        f32x4 bl[MR];
+        bias_tile(bl);
+        epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bl);
       }
       ti += walk.step;
       grp = 0;
@@ -1299,7 +1314,8 @@ static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& 
   if (ceil_div(g.pinst, NW) > maxit) return false;
   const size_t wb = (size_t)16 * MR * a.k * a.k * 64;
   // two stages: the next (tile, chunk group) streams in during the current one
-  smem = (c.resw ? nch * wb : 0) + 2 * (size_t)g.G * (g.p_bytes + (c.resw ? 0 : wb));
+  smem = (c.resw ? nch * wb : 0) + 2 * (size_t)g.G * (g.p_bytes + (c.resw ? 0 : wb)) +
+         (a.in8 ? 0 : (size_t)16 * MR * 4);  // bf16: the block's bias
   return smem <= 160 * 1024;
 }
 
