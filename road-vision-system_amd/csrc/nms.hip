@@ -12,14 +12,13 @@
 //
 // Sort: 64-bit keys (~score_bits, anchor, slot) bitonic-sorted in LDS
 // (score desc, anchor asc == the stable order of rows in anchor order).
-// Two passes with the same code: nms_kernel<kSortSmall> sorts up to 4096
-// candidates in ~41 KB of LDS (so conv blocks still fit beside it when the
-// track stage overlaps the next forward); an image with more candidates is
-// flagged (out_n = -1) and redone by nms_kernel<kSortCap>, which keeps its
-// keys in the caller's workspace (global memory, ~10 KB of LDS) and whose
-// blocks exit at once for every unflagged image.  kSortCap = 65536 covers
-// every slot of the candidate layout (cap <= 65536), so no candidate is ever
-// dropped before the sort.  max_nms: after the sort only the first max_nms
+// One launch: an image with up to 4096 candidates sorts its keys in ~41 KB
+// of LDS (so conv blocks still fit beside it when the track stage overlaps
+// the next forward); an image with more keeps them in the caller's
+// workspace (global memory) -- the same code on either pointer (nms_body).
+// kSortCap = 65536 covers every slot of the candidate layout (cap <= 65536),
+// so no candidate is ever dropped before the sort.  (r04 ran the overflow
+// images in a second launch, one more dependent launch per call.)  max_nms: after the sort only the first max_nms
 // keys take part in the greedy pass -- Ultralytics' `if n > max_nms: x =
 // x[x[:, 4].argsort(descending=True)[:max_nms]]` (top max_nms by score; ties
 // resolved in anchor order like the stable sort of the oracle).
@@ -68,64 +67,39 @@ __device__ __forceinline__ bool suppresses(float4 bi, float ai, float4 bj, float
 constexpr int kSegBytes = ((kMaxSeg + 1) * 4 + 15) & ~15;
 static size_t nms_smem(int cap_keys, int max_det) {
   const size_t lds_keys = cap_keys > kSortSmall ? 0 : (size_t)cap_keys * 8;  // overflow: global
-  return lds_keys + kSegBytes + 64 * (16 + 4 + 8) + (size_t)max_det * (16 + 4 + 4);
+  return lds_keys + kSegBytes + 64 * (16 + 4 + 8) + (size_t)max_det * (16 + 4 + 4) + 64 * 4;
 }
 
-template <int CAP>
-__global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand,
-                                                   const int* __restrict__ seg_n, int nseg, int cap,
-                                                   float max_wh, double iou, int max_det,
-                                                   int max_nms, ScaleArgs sc, const uint32_t* __restrict__ keep4,
-                                                   float* __restrict__ out, int* __restrict__ out_n,
-                                                   int* __restrict__ cand_total,
-                                                   uint64_t* __restrict__ gkeys) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x;
-  // overflow pass: only the images the first pass flagged
-  constexpr bool kGlobal = CAP > kSortSmall;
-  if (kGlobal && out_n[b] != -1) return;
-  constexpr size_t kLdsKeys = kGlobal ? 0 : (size_t)CAP * 8;
-  uint64_t* keys = kGlobal ? gkeys + (size_t)b * CAP : (uint64_t*)smem;  // CAP
-  int* segoff = (int*)(smem + kLdsKeys);                  // kMaxSeg + 1: exclusive prefix + total
-  uint64_t* cmask = (uint64_t*)(smem + kLdsKeys + kSegBytes);  // 64
-  float4* cbox = (float4*)(cmask + 64);                   // chunk boxes (64)
-  float* carea = (float*)(cbox + 64);                     // 64
-  float4* kbox = (float4*)(carea + 64);                   // kept offset boxes (max_det)
-  float* karea = (float*)(kbox + max_det);                // max_det
-  int* kslot = (int*)(karea + max_det);                   // max_det
-  __shared__ int s_nkeep;
-  __shared__ int wsum[16];
+// LDS layout of nms_kernel: [keys (kSortSmall x 8 B; unused by an image
+// whose candidates exceed kSortSmall -- its keys go to the workspace)]
+// [segment prefix] [chunk masks / boxes / areas] [kept boxes / areas / slots]
+struct NmsLds {
+  int* segoff;     // kMaxSeg + 1: exclusive prefix + total
+  uint64_t* cmask;  // 64
+  float4* cbox;     // chunk boxes (64)
+  float* carea;     // 64
+  float4* kbox;     // kept offset boxes (max_det)
+  float* karea;     // max_det
+  int* kslot;       // max_det, then the current chunk's 64 slots
+};
 
-  const Cand* cb = cand + (size_t)b * cap;
-  // segment counts -> exclusive prefix (one segment per thread, nseg <= 1024)
-  int cnt = 0;
-  if (tid < nseg) cnt = min(max(seg_n[(size_t)b * nseg + tid], 0), 64);
-  int incl = cnt;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int v = __shfl_up(incl, off);
-    if ((tid & 63) >= off) incl += v;
-  }
-  if ((tid & 63) == 63) wsum[tid >> 6] = incl;
-  __syncthreads();
-  int wpre = 0;
-  for (int w = 0; w < (tid >> 6); ++w) wpre += wsum[w];
-  if (tid < nseg) segoff[tid] = wpre + incl - cnt;
-  if (tid == 0) {
-    int tot = 0;
-    for (int w = 0; w < 16; ++w) tot += wsum[w];
-    segoff[kMaxSeg] = tot;
-  }
-  __syncthreads();
-  int n = segoff[kMaxSeg];
-  if (cand_total && tid == 0) cand_total[b] = n;
-  if (CAP == kSortSmall && n > CAP) {  // redone by the overflow pass
-    if (tid == 0) out_n[b] = -1;
-    return;
-  }
-  // n <= nseg * 64 <= cap <= kSortCap (checked by the host entry): the
-  // overflow pass sorts every candidate
+// Sort the image's n candidates (keys in LDS or, past kSortSmall, in the
+// workspace: KEYS is the pointer's type), greedy NMS, scale_boxes + class
+// filter.  Every block thread calls it.
+template <class KEYS>
+__device__ void nms_body(KEYS* keys, int n, const NmsLds& L, const Cand* __restrict__ cb, int nseg,
+                         int b, float max_wh, double iou, int max_det, int max_nms, ScaleArgs sc,
+                         const uint32_t* __restrict__ keep4, float* __restrict__ out,
+                         int* __restrict__ out_n) {
+  const int tid = threadIdx.x;
+  int* segoff = L.segoff;
+  uint64_t* cmask = L.cmask;
+  float4* cbox = L.cbox;
+  float* carea = L.carea;
+  float4* kbox = L.kbox;
+  float* karea = L.karea;
+  int* kslot = L.kslot;
+  __shared__ int s_nkeep;
   int np2 = 1;
   while (np2 < n) np2 <<= 1;
   for (int i = tid; i < np2; i += blockDim.x) keys[i] = ~0ull;
@@ -141,6 +115,18 @@ __global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand
     }
   }
   __syncthreads();
+  if (n <= (int)blockDim.x) {
+    // rank sort: thread i's key lands at the number of smaller keys (keys
+    // are unique: the slot is in the low bits); every thread reads the
+    // same key at the same time (an LDS broadcast), so n keys cost n reads
+    // and two barriers instead of log2(np2)^2 / 2 bitonic stages
+    const uint64_t mine = tid < n ? keys[tid] : ~0ull;
+    int r = 0;
+    for (int j = 0; j < n; ++j) r += keys[j] < mine ? 1 : 0;
+    __syncthreads();
+    if (tid < n) keys[r] = mine;
+    __syncthreads();
+  } else
   // bitonic sort ascending
   for (int size = 2; size <= np2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -159,55 +145,84 @@ __global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand
   }
   // Ultralytics max_nms: only the top max_nms by score enter torchvision nms
   if (n > max_nms) n = max_nms;
-  // greedy NMS on wave 0
-  if (tid < 64) {
-    const int lane = tid;
-    int nkeep = 0;
-    for (int base = 0; base < n && nkeep < max_det; base += 64) {
+  // greedy NMS, chunks of 64 candidates (score order), all 16 waves:
+  //  1. wave 0 fetches the chunk's boxes into LDS and clears the chunk masks;
+  //  2. wave w tests every chunk candidate (its lane) against the kept boxes
+  //     k = w, w + 16, ... (suppressed flags -> one ballot per wave) and
+  //     against the later chunk members j = w, w + 16, ... (bits of the
+  //     lane's chunk mask, OR-ed into LDS);
+  //  3. wave 0 resolves the chunk in order -- q kept iff still alive, then
+  //     q's mask kills the later members it overlaps -- with every mask in a
+  //     register (read across lanes by readlane, no LDS round trip per q).
+  // Same decisions as one wave walking each candidate against every kept
+  // box (r04): the IoU test is symmetric, order only matters in step 3.
+  // (r04's single-wave form paid a serial LDS read per kept box and per
+  // chunk member: 48 us for an image of 129 candidates.)
+  __shared__ uint64_t supw[16];
+  const int lane = tid & 63, wv = tid >> 6;
+  const int nwv = blockDim.x >> 6;
+  if (tid == 0) s_nkeep = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += 64) {
+    const int nkeep = s_nkeep;
+    if (nkeep >= max_det) break;  // uniform: read after the last barrier
+    if (wv == 0) {
       const int i = base + lane;
-      const bool valid = i < n;
       float4 bx = make_float4(0.f, 0.f, 0.f, 0.f);
       float ar = 0.f;
-      int slot = 0;
-      if (valid) {
+      int slot = -1;
+      if (i < n) {
         slot = (int)(keys[i] & 0xFFFF);
         bx = offset_box(cb[slot], max_wh);
         ar = (bx.z - bx.x) * (bx.w - bx.y);
       }
-      bool sup = !valid;
-      for (int k = 0; k < nkeep && !sup; ++k) sup = suppresses(kbox[k], karea[k], bx, ar, iou);
       cbox[lane] = bx;
       carea[lane] = ar;
-      wave_sync();
+      cmask[lane] = 0;
+      kslot[max_det + lane] = slot;  // staged: the chunk's slots (kslot has max_det + 64 entries)
+    }
+    __syncthreads();
+    {
+      const bool valid = base + lane < n;
+      const float4 bx = cbox[lane];
+      const float ar = carea[lane];
+      bool sup = !valid;
+      for (int k = wv; k < nkeep && !sup; k += nwv) sup = suppresses(kbox[k], karea[k], bx, ar, iou);
+      const uint64_t bal = __ballot(sup);
+      if (lane == 0) supw[wv] = bal;
       uint64_t m = 0;
-      if (valid) {
-        for (int j = lane + 1; j < 64 && base + j < n; ++j)
-          if (suppresses(bx, ar, cbox[j], carea[j], iou)) m |= 1ull << j;
-      }
-      cmask[lane] = m;
-      wave_sync();
-      uint64_t alive = __ballot(!sup);
+      if (valid)
+        for (int j = wv; j < 64 && base + j < n; j += nwv)
+          if (j > lane && suppresses(bx, ar, cbox[j], carea[j], iou)) m |= 1ull << j;
+      if (m) atomicOr((unsigned long long*)&cmask[lane], (unsigned long long)m);
+    }
+    __syncthreads();
+    if (wv == 0) {
+      uint64_t supall = 0;
+      for (int w = 0; w < nwv; ++w) supall |= supw[w];
+      uint64_t alive = ~supall;
+      const uint64_t mine = cmask[lane];
+      const uint32_t mlo = (uint32_t)mine, mhi = (uint32_t)(mine >> 32);
       uint64_t kept = 0;
       int room = max_det - nkeep;
-      for (int q = 0; q < 64 && room > 0; ++q) {
-        if ((alive >> q) & 1ull) {
-          kept |= 1ull << q;
-          alive &= ~cmask[q];
-          --room;
-        }
+      while (alive && room > 0) {  // uniform
+        const int q = __builtin_ctzll(alive);
+        kept |= 1ull << q;
+        const uint64_t mq = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(mhi, q) << 32) |
+                            (uint64_t)(uint32_t)__builtin_amdgcn_readlane(mlo, q);
+        alive &= ~(mq | (1ull << q));
+        --room;
       }
       if ((kept >> lane) & 1ull) {
         const int pos = nkeep + __popcll(kept & ((1ull << lane) - 1ull));
-        kbox[pos] = bx;
-        karea[pos] = ar;
-        kslot[pos] = slot;
+        kbox[pos] = cbox[lane];
+        karea[pos] = carea[lane];
+        kslot[pos] = kslot[max_det + lane];
       }
-      nkeep += __popcll(kept);
-      wave_sync();
+      if (lane == 0) s_nkeep = nkeep + __popcll(kept);
     }
-    if (lane == 0) s_nkeep = nkeep;
+    __syncthreads();
   }
-  __syncthreads();
   // scale_boxes + clip + post-NMS class filter, order preserved
   if (tid < 64) {
     const int nkeep = s_nkeep;
@@ -241,6 +256,63 @@ __global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand
     }
     if (tid == 0) out_n[b] = w;
   }
+}
+
+// One workgroup per image: segment prefix, then nms_body with the keys in
+// LDS (n <= kSortSmall: ~41 KB of LDS, so conv blocks still fit beside it
+// when the track stage overlaps the next forward) or in the workspace
+// (kSortCap = 65536 covers every slot of the candidate layout, so no
+// candidate is ever dropped before the sort) -- one launch either way.
+__global__ __launch_bounds__(1024) void nms_kernel(const Cand* __restrict__ cand,
+                                                   const int* __restrict__ seg_n, int nseg, int cap,
+                                                   float max_wh, double iou, int max_det,
+                                                   int max_nms, ScaleArgs sc, const uint32_t* __restrict__ keep4,
+                                                   float* __restrict__ out, int* __restrict__ out_n,
+                                                   int* __restrict__ cand_total,
+                                                   uint64_t* __restrict__ gkeys) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  constexpr size_t kLdsKeys = (size_t)kSortSmall * 8;
+  NmsLds L;
+  L.segoff = (int*)(smem + kLdsKeys);
+  L.cmask = (uint64_t*)(smem + kLdsKeys + kSegBytes);
+  L.cbox = (float4*)(L.cmask + 64);
+  L.carea = (float*)(L.cbox + 64);
+  L.kbox = (float4*)(L.carea + 64);
+  L.karea = (float*)(L.kbox + max_det);
+  L.kslot = (int*)(L.karea + max_det);
+  int* segoff = L.segoff;
+  __shared__ int wsum[16];
+  const Cand* cb = cand + (size_t)b * cap;
+  // segment counts -> exclusive prefix (one segment per thread, nseg <= 1024)
+  int cnt = 0;
+  if (tid < nseg) cnt = min(max(seg_n[(size_t)b * nseg + tid], 0), 64);
+  int incl = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_up(incl, off);
+    if ((tid & 63) >= off) incl += v;
+  }
+  if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+  __syncthreads();
+  int wpre = 0;
+  for (int w = 0; w < (tid >> 6); ++w) wpre += wsum[w];
+  if (tid < nseg) segoff[tid] = wpre + incl - cnt;
+  if (tid == 0) {
+    int tot = 0;
+    for (int w = 0; w < 16; ++w) tot += wsum[w];
+    segoff[kMaxSeg] = tot;
+  }
+  __syncthreads();
+  const int n = segoff[kMaxSeg];
+  if (cand_total && tid == 0) cand_total[b] = n;
+  // n <= nseg * 64 <= cap <= kSortCap (checked by the host entry)
+  if (n <= kSortSmall)
+    nms_body((uint64_t*)smem, n, L, cb, nseg, b, max_wh, iou, max_det, max_nms, sc, keep4, out, out_n);
+  else
+    nms_body(gkeys + (size_t)b * kSortCap, n, L, cb, nseg, b, max_wh, iou, max_det, max_nms, sc, keep4,
+             out, out_n);
 }
 
 // Reference-layout candidates: raw (B, 4+nc, A) -> Cand rows (xc filter,
@@ -320,13 +392,8 @@ extern "C" int rv_nms_postprocess(const void* cand, const int* seg_n, int B, int
   sc.clip_h = scale5[4];
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)nms_kernel<kSortCap>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)rv_nms_smem_bytes());
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)nms_kernel<kSortSmall>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)nms_smem(kSortSmall, kMaxDet));
     if (e != hipSuccess) {
       set_error("hipFuncSetAttribute(NMS LDS): %s", hipGetErrorString(e));
       (void)hipGetLastError();
@@ -334,15 +401,10 @@ extern "C" int rv_nms_postprocess(const void* cand, const int* seg_n, int B, int
     }
     attr = true;
   }
-  nms_kernel<kSortSmall><<<B, 1024, nms_smem(kSortSmall, max_det), as_stream(stream)>>>(
-      (const Cand*)cand, seg_n, nseg, cap, max_wh, (double)iou, max_det, max_nms, sc, keep_mask4,
-      out, out_n, cand_total, nullptr);
-  int st = launch_status("rv_nms_postprocess");
-  if (st) return st;
-  nms_kernel<kSortCap><<<B, 1024, nms_smem(kSortCap, max_det), as_stream(stream)>>>(
+  nms_kernel<<<B, 1024, nms_smem(kSortSmall, max_det), as_stream(stream)>>>(
       (const Cand*)cand, seg_n, nseg, cap, max_wh, (double)iou, max_det, max_nms, sc, keep_mask4,
       out, out_n, cand_total, (uint64_t*)ws);
-  return launch_status("rv_nms_postprocess (overflow pass)");
+  return launch_status("rv_nms_postprocess");
 }
 
 extern "C" int rv_cand_segments(int A) { return A > 0 ? ceil_div(A, 64) : 0; }
