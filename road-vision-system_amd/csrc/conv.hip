@@ -1286,16 +1286,32 @@ static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& 
   // tile width: the fewest halo-patch pixels DMA'd over the whole layer
   // (tiles x PH x PW, edge tiles included); at least 16 columns, so a B
   // fragment's 16 pixels mostly share one patch row (conflict-free reads)
+  // (the search runs up to ~300 candidates with four divisions each; a plan
+  // asks for the same few shapes on every forward, so the answers are kept:
+  // host time per launch matters at batch 1, where the kernels are ~5 us)
+  struct TileKey {
+    int wo, ho, s, k, p, c;
+  };
+  static thread_local TileKey memo[64];
+  static thread_local int memo_n = 0, memo_w = 0;
   int C = 0;
-  long best = -1;
-  for (int c = std::min(a.Wo, P); c >= std::min(16, a.Wo); --c) {
-    const int r = P / c;
-    const long cost = (long)ceil_div(a.Wo, c) * ceil_div(a.Ho, r) * ((r - 1) * a.stride + a.k) *
-                      ((c - 1) * a.stride + a.k);
-    if (best < 0 || cost < best) {
-      best = cost;
-      C = c;
+  for (int i = 0; i < memo_n && !C; ++i)
+    if (memo[i].wo == a.Wo && memo[i].ho == a.Ho && memo[i].s == a.stride && memo[i].k == a.k &&
+        memo[i].p == P)
+      C = memo[i].c;
+  if (!C) {
+    long best = -1;
+    for (int c = std::min(a.Wo, P); c >= std::min(16, a.Wo); --c) {
+      const int r = P / c;
+      const long cost = (long)ceil_div(a.Wo, c) * ceil_div(a.Ho, r) * ((r - 1) * a.stride + a.k) *
+                        ((c - 1) * a.stride + a.k);
+      if (best < 0 || cost < best) {
+        best = cost;
+        C = c;
+      }
     }
+    memo[memo_w++ & 63] = TileKey{a.Wo, a.Ho, a.stride, a.k, P, C};
+    memo_n = std::min(memo_n + 1, 64);
   }
   g.C = C;
   g.R = P / C;

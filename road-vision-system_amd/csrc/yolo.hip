@@ -1201,8 +1201,11 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
   static const int streams_env = getenv("RV_HEAD_STREAMS") ? atoi(getenv("RV_HEAD_STREAMS")) != 0 : -1;
   const bool streams_on = streams_env >= 0 ? streams_env != 0 : M->head_streams != 0;
   // profiled forwards time every launch alone (per-launch roofline), so the
-  // heads stay on the caller's stream there
-  const bool fork = streams_on && M->side[0] && M->side[1] &&
+  // heads stay on the caller's stream there; so do batches under 8, whose
+  // few-us head launches gain less from the overlap than the fork / join
+  // event round trips cost (batch 1, r05: 0.356 -> 0.308 ms device time per
+  // forward, launch submission 284 -> 218 us, tools/c2_host.py)
+  const bool fork = streams_on && B >= 8 && M->side[0] && M->side[1] &&
                     !(M->prof.on && M->prof.n_fwd < M->prof.cap_fwd);
   const hipStream_t main_s = E.s;
   auto head_level = [&](int i) {

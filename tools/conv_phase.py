@@ -16,12 +16,14 @@ from rvs_amd.detect import weights  # noqa: E402
 from rvs_amd.detect.yolo_hip import YoloEngine  # noqa: E402
 
 B = int(os.environ.get("B", 128))
-eng = YoloEngine(0, weights.synthetic_weights(0), B, (1080, 1920), imgsz=640)
-x = (torch.rand((B, 1080, 1920, 3), device="cuda") * 255).to(torch.uint8)
+H, W = int(os.environ.get("H", 1080)), int(os.environ.get("W", 1920))
+eng = YoloEngine(0, weights.synthetic_weights(0), B, (H, W), imgsz=640)
+x = (torch.rand((B, H, W, 3), device="cuda") * 255).to(torch.uint8)
 lb = eng.letterbox(x)
 eng.forward_raw(lb)
 eng.autotune(lb)
-eng.load_tuned([tuple(c[:4]) + (1,) + tuple(c[5:]) for c in eng.tuned_configs()])
+if not os.environ.get("KEEP_PERSIST"):  # B=1: keep the tuned grids
+    eng.load_tuned([tuple(c[:4]) + (1,) + tuple(c[5:]) for c in eng.tuned_configs()])
 lib = _lib.load()
 f = lib.rv_conv_phase_read
 f.argtypes = [ctypes.c_void_p, ctypes.c_int]

@@ -35,6 +35,18 @@ def report(path, n):
           f"{len(win) / n:.1f} dispatches per call")
     for k, (c, us) in sorted(per.items(), key=lambda x: -x[1][1]):
         print(f"  {k:32s} {c / n:5.1f}/call {us / n:7.1f} us/call {us / c:6.2f} us avg")
+    # the last call, dispatch by dispatch (duration, gap to the previous end, grid)
+    per_call = len(win) // n
+    prev = None
+    print("last call:")
+    for r in win[-per_call:]:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        gap = (s - prev) / 1e3 if prev is not None else 0.0
+        prev = e
+        k = r["Kernel_Name"].split("(")[0].replace("void rv::", "").split("<")[0]
+        grid = r.get("Grid_Size_X", r.get("Grid_Size", "?"))
+        wg = r.get("Workgroup_Size_X", r.get("Workgroup_Size", "?"))
+        print(f"  {(e - s) / 1e3:7.2f} us  gap {gap:6.2f}  grid {grid:>7} wg {wg:>5}  {k}")
 
 
 def main():
