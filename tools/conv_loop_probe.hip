@@ -128,6 +128,13 @@ int main(int argc, char** argv) {
   const int ncu = 256, iters = argc > 1 ? atoi(argv[1]) : 2000;
   hipMalloc(&g_src, kSrcBytes);
   hipMemset(g_src, 0, kSrcBytes);
+  // the loop alone: no DMA (barrier every chunk step, or none)
+  g_src_bytes = 2u << 20;
+  run<4, 2, 4, false>(ncu, iters);
+  run<4, 2, 4, true>(ncu, iters);
+  run<5, 2, 8, true>(ncu, iters);
+  run<2, 2, 8, true>(ncu, iters);
+  run<2, 1, 4, true>(ncu, iters);
   for (int pass = 0; pass < 2; ++pass) {
     g_src_bytes = pass == 0 ? (256u << 20) : (2u << 20);
     run<5, 2, 8, true, 3>(ncu, iters);
