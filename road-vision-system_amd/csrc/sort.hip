@@ -275,7 +275,10 @@ __device__ void track_init(Track& t, int id, const float* det, double ts) {
 // the new tracks that do not fit (their ids are still handed out) and sets
 // the stream's sticky overflow flag (rv_sort_stats).
 // ---------------------------------------------------------------------------
-constexpr int kAssocThreads = 1024;
+#ifndef RV_ASSOC_THREADS
+#define RV_ASSOC_THREADS 1024
+#endif
+constexpr int kAssocThreads = RV_ASSOC_THREADS;
 
 struct SortWs {  // per-frame workspace views (rv_sort_ws_bytes)
   float* M;         // S x tmax x dmax IoU matrix (argmax fallback only)
@@ -408,12 +411,27 @@ __global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
 
   // ---- association (_associate, sort_tracker.py:182-210)
   if (T > 0 && D > 0) {
-    for (int i = tid; i < T * D; i += kAssocThreads) {
-      const int t = i / D, d = i - (i / D) * D;
-      const float v = iou_f32(tbox[t], dbox[d]);
-      if ((double)v >= p.iou_thr) {
-        const int k = atomicAdd(&s_cnt, 1);
-        if (k < kKeyCap) keys[k] = ((uint64_t)(~__float_as_uint(v)) << 32) | (uint64_t)(uint32_t)i;
+    // qualifying pairs appended with one LDS atomic per wave (a ballot's
+    // popcount), not one per pair; the append order does not matter (the
+    // keys are sorted next and unique)
+    for (int i0 = 0; i0 < T * D; i0 += kAssocThreads) {
+      const int i = i0 + tid;
+      bool q = false;
+      float v = 0.f;
+      if (i < T * D) {
+        const int t = i / D, d = i - (i / D) * D;
+        v = iou_f32(tbox[t], dbox[d]);
+        q = (double)v >= p.iou_thr;
+      }
+      const unsigned long long m = __ballot(q);
+      if (m) {  // wave-uniform
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&s_cnt, __popcll(m));
+        base = __shfl(base, 0);
+        if (q) {
+          const int k = base + __popcll(m & ((1ull << lane) - 1ull));
+          if (k < kKeyCap) keys[k] = ((uint64_t)(~__float_as_uint(v)) << 32) | (uint64_t)(uint32_t)i;
+        }
       }
     }
     __syncthreads();
@@ -421,6 +439,19 @@ __global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
     if (cnt <= kKeyCap) {
       int np2 = 1;
       while (np2 < cnt) np2 <<= 1;
+      if (cnt <= kAssocThreads) {
+        // rank sort: key i lands at the number of smaller keys (unique:
+        // the flat index is in the low bits); every thread reads the same
+        // key at once (an LDS broadcast) -- cnt reads and two barriers
+        // instead of log2(np2)^2 / 2 bitonic stages
+        const uint64_t mine = tid < cnt ? keys[tid] : ~0ull;
+        int r = 0;
+        for (int j = 0; j < cnt; ++j) r += keys[j] < mine ? 1 : 0;
+        __syncthreads();
+        if (tid < cnt) keys[r] = mine;
+        __syncthreads();
+        np2 = 0;  // sorted
+      }
       for (int i = cnt + tid; i < np2; i += kAssocThreads) keys[i] = ~0ull;
       __syncthreads();
       for (int size = 2; size <= np2; size <<= 1)
