@@ -117,19 +117,32 @@ __device__ __forceinline__ void c2f_conv3(const uint8_t* __restrict__ in, uint8_
 #pragma unroll
       for (int m = 0; m < MR; ++m) acc[n][m] = f32x4c{0.f, 0.f, 0.f, 0.f};
     }
+    // B fragments read D - 1 taps ahead into a ring of registers, the order
+    // pinned by sched_barrier fences: left to the scheduler, every tap's
+    // ds_read_b128 landed in one register right before its MFMA with an
+    // lgkmcnt(0) wait in between -- 18 serial LDS round trips per fragment
+    // pair.  The MFMA order (taps ascending, then n, then m) is unchanged.
+    constexpr int D = 4;
+    bf16x8c Bq[D][2];
+    auto ld = [&](int t, int sl) {
+      const int ky = t / 3, kx = t - (t / 3) * 3;
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+      for (int n = 0; n < 2; ++n)
+        Bq[sl][n] = __builtin_bit_cast(bf16x8c, *(const uint4*)(bp[n] + (ky * rwi + kx) * G::PB));
+    };
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
+    for (int t = 0; t < D - 1; ++t) ld(t, t);
 #pragma unroll
-        for (int n = 0; n < 2; ++n) {
-          const uint4 b = *(const uint4*)(bp[n] + (ky * rwi + kx) * G::PB);
-          const bf16x8c B = __builtin_bit_cast(bf16x8c, b);
+    for (int t = 0; t < 9; ++t) {
+      if (t + D - 1 < 9) ld(t + D - 1, (t + D - 1) % D);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int m = 0; m < MR; ++m)
-            acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ky * 3 + kx][m], B, acc[n][m], 0, 0, 0);
-        }
-      }
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int m = 0; m < MR; ++m)
+          acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[t][m], Bq[t % D][n], acc[n][m], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
       if (o[n] >= rpo) continue;
@@ -258,6 +271,9 @@ __global__ __launch_bounds__(512) void c2f_chain_kernel(C2fArgs a) {
     for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int m = 0; m < MR2; ++m) acc[n][m] = f32x4c{0.f, 0.f, 0.f, 0.f};
+    // every k-step's B fragments first (NCH x 2 ds_read_b128 in flight),
+    // then the MFMAs in the same order as before
+    bf16x8c B2[NCH][2];
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
       const int k0 = j * 32 + quad * 8;  // first concat channel of this lane's k-slice
@@ -272,12 +288,17 @@ __global__ __launch_bounds__(512) void c2f_chain_kernel(C2fArgs a) {
           const int p = (r + e) * T::rw(e) + c + e;
           bq = *(const uint4*)(smem + seg_buf(s) + G::addr(p, qq));
         }
-        const bf16x8c B = __builtin_bit_cast(bf16x8c, bq);
-#pragma unroll
-        for (int m = 0; m < MR2; ++m)
-          acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2[j][m], B, acc[n][m], 0, 0, 0);
+        B2[j][n] = __builtin_bit_cast(bf16x8c, bq);
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int m = 0; m < MR2; ++m)
+          acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2[j][m], B2[j][n], acc[n][m], 0, 0, 0);
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
       const int o = (f0 + n) * 16 + col;
