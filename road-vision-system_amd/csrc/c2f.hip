@@ -191,36 +191,36 @@ __global__ __launch_bounds__(512) void c2f_chain_kernel(C2fArgs a) {
   const int oy0 = ty * TR, ox0 = tx * TC;
   const bf16_t* img = a.cat + (size_t)b * a.H * a.W * a.cat_cs + a.cat_co;
 
-  // ---- 1. y1 (halo h) and y0 (tile) from the concat buffer, zero outside
+  // ---- 1. y1 (halo h) and y0 (tile) from the concat buffer, zero outside.
+  //      Element i of a map is its 16-B quarter i % NQ of pixel i / NQ, stored
+  //      at byte 16 i (PB = 16 NQ); the map widths are compile-time, so the
+  //      pixel's (row, column) is a division by a constant, and every load of
+  //      a thread is issued before the first LDS store.
   {
     constexpr int NY = T::rp(h) * G::NQ, N0 = T::rp(0) * G::NQ;
-    constexpr int NT = NY + N0;
-    constexpr int IT = 4;  // loads in flight per thread
-    for (int i0 = tid; i0 < NT; i0 += 512 * IT) {
-      uint4 v[IT];
-      int dst[IT];
-#pragma unroll
-      for (int u = 0; u < IT; ++u) {
-        const int i = i0 + u * 512;
-        v[u] = make_uint4(0, 0, 0, 0);
-        dst[u] = -1;
-        if (i < NT) {
-          const bool is1 = i < NY;
-          const int j = is1 ? i : i - NY;
-          const int p = j / G::NQ, q = j - p * G::NQ;
-          const int e = is1 ? h : 0;
-          const int rwe = T::rw(e);
-          const int r = p / rwe, c = p - r * rwe;
-          const int gy = oy0 - e + r, gx = ox0 - e + c;
-          dst[u] = (is1 ? L::Y : L::Y0) + G::addr(p, q);
-          if ((unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W)
-            v[u] = *(const uint4*)(img + ((size_t)gy * a.W + gx) * a.cat_cs + (is1 ? C : 0) + q * 8);
-        }
+    constexpr int U1 = (NY + 511) / 512, U0 = (N0 + 511) / 512;
+    auto fetch = [&](int i, int n, int e, int rwe, int ch) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (i < n) {
+        const int p = i / G::NQ, q = i - p * G::NQ;
+        const int r = p / rwe, c = p - r * rwe;
+        const int gy = oy0 - e + r, gx = ox0 - e + c;
+        if ((unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W)
+          v = *(const uint4*)(img + (size_t)((gy * a.W + gx) * a.cat_cs + ch + q * 8));
       }
+      return v;
+    };
+    uint4 v1[U1], v0[U0];
 #pragma unroll
-      for (int u = 0; u < IT; ++u)
-        if (dst[u] >= 0) *(uint4*)(smem + dst[u]) = v[u];
-    }
+    for (int u = 0; u < U1; ++u) v1[u] = fetch(tid + 512 * u, NY, h, T::rw(h), C);
+#pragma unroll
+    for (int u = 0; u < U0; ++u) v0[u] = fetch(tid + 512 * u, N0, 0, T::rw(0), 0);
+#pragma unroll
+    for (int u = 0; u < U1; ++u)
+      if (tid + 512 * u < NY) *(uint4*)(smem + L::Y + 16 * (tid + 512 * u)) = v1[u];
+#pragma unroll
+    for (int u = 0; u < U0; ++u)
+      if (tid + 512 * u < N0) *(uint4*)(smem + L::Y0 + 16 * (tid + 512 * u)) = v0[u];
     for (int i = tid; i < L::ZBYTES / 16; i += 512) *(uint4*)(smem + L::ZR + 16 * i) = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
