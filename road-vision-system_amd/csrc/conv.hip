@@ -997,6 +997,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
               }
 #pragma unroll
               for (int n = 0; n < NR; ++n) Bf[n] = *(const long*)(Prow + (boff[n][kx] ^ (hh << 5)));
+              // every read of the tap issued before its MFMAs (left alone,
+              // the scheduler waits for each A fragment right before its
+              // MFMAs: one LDS round trip per m)
+              __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
               for (int m = 0; m < MR; ++m)
 #pragma unroll
@@ -1014,6 +1018,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
 #pragma unroll
             for (int n = 0; n < NR; ++n)
               Bf[n] = __builtin_bit_cast(bf16x8, *(const uint4*)(Prow + boff[n][kx]));
+            // every read of the tap issued before its MFMAs (left alone, the
+            // scheduler waits for each A fragment right before its MFMAs:
+            // one LDS round trip per m)
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int m = 0; m < MR; ++m)
 #pragma unroll
