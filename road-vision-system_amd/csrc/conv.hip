@@ -1777,12 +1777,17 @@ __global__ __launch_bounds__(256) void sppf_pool_kernel(uint8_t* __restrict__ bu
     float a5[NV], a9[NV], a13[NV];
 #pragma unroll
     for (int j = 0; j < NV; ++j) a5[j] = a9[j] = a13[j] = -INFINITY;
+    // the 13 taps' LDS reads all issued first (a branch around each read
+    // made every one a separate LDS round trip); out-of-map taps read the
+    // edge pixel instead, which the window always holds, so the max (the
+    // -inf padding of MaxPool2d) is unchanged
+    uint4 raw[13];
+#pragma unroll
+    for (int d = -6; d <= 6; ++d) raw[d + 6] = xs[y * W + min(max(x + d, 0), W - 1)];
 #pragma unroll
     for (int d = -6; d <= 6; ++d) {
-      const int xx = x + d;
-      if (xx < 0 || xx >= W) continue;
       float f[NV];
-      V::dec(xs[y * W + xx], f);
+      V::dec(raw[d + 6], f);
 #pragma unroll
       for (int j = 0; j < NV; ++j) {
         a13[j] = fmaxf(a13[j], f[j]);
@@ -1800,26 +1805,23 @@ __global__ __launch_bounds__(256) void sppf_pool_kernel(uint8_t* __restrict__ bu
     float a5[NV], a9[NV], a13[NV];
 #pragma unroll
     for (int j = 0; j < NV; ++j) a5[j] = a9[j] = a13[j] = -INFINITY;
+    // column pass, the same way: each map's taps read first, edge rows
+    // standing in for the out-of-map ones
+    auto col_max = [&](const uint4* hm, int r, float (&acc)[NV]) {
+      uint4 rv[13];
 #pragma unroll
-    for (int d = -6; d <= 6; ++d) {
-      const int yy = y + d;
-      if (yy < 0 || yy >= H) continue;
-      const int q = yy * W + x;
-      float f[NV];
-      V::dec(h13[q], f);
+      for (int d = -r; d <= r; ++d) rv[d + r] = hm[min(max(y + d, 0), H - 1) * W + x];
 #pragma unroll
-      for (int j = 0; j < NV; ++j) a13[j] = fmaxf(a13[j], f[j]);
-      if (d >= -4 && d <= 4) {
-        V::dec(h9[q], f);
+      for (int d = 0; d <= 2 * r; ++d) {
+        float f[NV];
+        V::dec(rv[d], f);
 #pragma unroll
-        for (int j = 0; j < NV; ++j) a9[j] = fmaxf(a9[j], f[j]);
+        for (int j = 0; j < NV; ++j) acc[j] = fmaxf(acc[j], f[j]);
       }
-      if (d >= -2 && d <= 2) {
-        V::dec(h5[q], f);
-#pragma unroll
-        for (int j = 0; j < NV; ++j) a5[j] = fmaxf(a5[j], f[j]);
-      }
-    }
+    };
+    col_max(h13, 6, a13);
+    col_max(h9, 4, a9);
+    col_max(h5, 2, a5);
     uint8_t* o = img + (size_t)p * cs;
     *(uint4*)(o + c * EB) = V::enc(a5);
     *(uint4*)(o + 2 * c * EB) = V::enc(a9);
