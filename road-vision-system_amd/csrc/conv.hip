@@ -1246,6 +1246,9 @@ __global__ __launch_bounds__(256, 2) void conv1x1_direct_kernel(ConvArgs a, int 
       bf16x8 A[MR];
 #pragma unroll
       for (int m = 0; m < MR; ++m) A[m] = __builtin_bit_cast(bf16x8, *(const uint4*)(Wl + aoff[m]));
+      // all MR weight reads in flight before the first MFMA (left alone, the
+      // scheduler waits for each A fragment right before its MFMAs)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int m = 0; m < MR; ++m)
 #pragma unroll
