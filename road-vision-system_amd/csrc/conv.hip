@@ -1780,22 +1780,27 @@ __global__ __launch_bounds__(256) void sppf_pool_kernel(uint8_t* __restrict__ bu
     float a5[NV], a9[NV], a13[NV];
 #pragma unroll
     for (int j = 0; j < NV; ++j) a5[j] = a9[j] = a13[j] = -INFINITY;
-    // the 13 taps' LDS reads all issued first (a branch around each read
-    // made every one a separate LDS round trip); out-of-map taps read the
-    // edge pixel instead, which the window always holds, so the max (the
-    // -inf padding of MaxPool2d) is unchanged
-    uint4 raw[13];
+    // the taps' LDS reads issued in two groups (7 + 6) ahead of their max
+    // chains (a branch around each read made every one a separate LDS round
+    // trip; all 13 at once doubled the VGPRs, which cost more beside the
+    // forward's other kernels than the round trips saved); out-of-map taps
+    // read the edge pixel instead, which the window always holds, so the
+    // max (the -inf padding of MaxPool2d) is unchanged
 #pragma unroll
-    for (int d = -6; d <= 6; ++d) raw[d + 6] = xs[y * W + min(max(x + d, 0), W - 1)];
+    for (int d0 = -6; d0 <= 6; d0 += 7) {
+      uint4 raw[7];
 #pragma unroll
-    for (int d = -6; d <= 6; ++d) {
-      float f[NV];
-      V::dec(raw[d + 6], f);
+      for (int d = d0; d < d0 + 7 && d <= 6; ++d) raw[d - d0] = xs[y * W + min(max(x + d, 0), W - 1)];
 #pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        a13[j] = fmaxf(a13[j], f[j]);
-        if (d >= -4 && d <= 4) a9[j] = fmaxf(a9[j], f[j]);
-        if (d >= -2 && d <= 2) a5[j] = fmaxf(a5[j], f[j]);
+      for (int d = d0; d < d0 + 7 && d <= 6; ++d) {
+        float f[NV];
+        V::dec(raw[d - d0], f);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          a13[j] = fmaxf(a13[j], f[j]);
+          if (d >= -4 && d <= 4) a9[j] = fmaxf(a9[j], f[j]);
+          if (d >= -2 && d <= 2) a5[j] = fmaxf(a5[j], f[j]);
+        }
       }
     }
     h5[p] = V::enc(a5);
@@ -1811,15 +1816,18 @@ __global__ __launch_bounds__(256) void sppf_pool_kernel(uint8_t* __restrict__ bu
     // column pass, the same way: each map's taps read first, edge rows
     // standing in for the out-of-map ones
     auto col_max = [&](const uint4* hm, int r, float (&acc)[NV]) {
-      uint4 rv[13];
 #pragma unroll
-      for (int d = -r; d <= r; ++d) rv[d + r] = hm[min(max(y + d, 0), H - 1) * W + x];
+      for (int d0 = -r; d0 <= r; d0 += 7) {
+        uint4 rv[7];
 #pragma unroll
-      for (int d = 0; d <= 2 * r; ++d) {
-        float f[NV];
-        V::dec(rv[d], f);
+        for (int d = d0; d < d0 + 7 && d <= r; ++d) rv[d - d0] = hm[min(max(y + d, 0), H - 1) * W + x];
 #pragma unroll
-        for (int j = 0; j < NV; ++j) acc[j] = fmaxf(acc[j], f[j]);
+        for (int d = d0; d < d0 + 7 && d <= r; ++d) {
+          float f[NV];
+          V::dec(rv[d - d0], f);
+#pragma unroll
+          for (int j = 0; j < NV; ++j) acc[j] = fmaxf(acc[j], f[j]);
+        }
       }
     };
     col_max(h13, 6, a13);
