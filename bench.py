@@ -110,8 +110,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-frames", type=int, default=int(os.environ.get("RV_CPU_FRAMES", 12)),
                     help="CPU baseline: frames per worker (one camera stream per worker)")
     ap.add_argument("--cpu-workers", type=int, default=int(os.environ.get("RV_CPU_WORKERS", 0)),
-                    help="CPU baseline workers (0: OMP_NUM_THREADS, else the CPUs this process "
-                         "may run on)")
+                    help="CPU baseline workers (0: the CPUs this process may use: its affinity "
+                         "mask capped by the cgroup CPU quota, host_cpu_budget)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the pair-1 rate and the secondary legs (configs[1], configs[4], "
@@ -564,6 +564,35 @@ def host_cpu_model() -> str:
     return "unknown"
 
 
+def host_cpu_budget() -> dict:
+    """The CPUs this process can actually use: its affinity mask, capped by
+    the cgroup CPU quota when one is set (cgroup v2 cpu.max, or v1
+    cpu.cfs_quota_us / cfs_period_us).  On the GPU box the mask lists all
+    256 host CPUs but cpu.max grants 16 CPUs' worth of time, so more than 16
+    single-threaded workers would only time-share those 16."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None and int(quota) < aff:
+        n = max(1, int(quota))
+        return {"cpus": n, "quota_cpus": round(quota, 2),
+                "reason": f"cgroup CPU quota = {quota:g} CPUs of the {aff} in the affinity mask: "
+                          f"one single-threaded worker per quota CPU"}
+    return {"cpus": aff, "quota_cpus": None if quota is None else round(quota, 2),
+            "reason": f"all {aff} CPUs of the affinity mask (no tighter cgroup CPU quota)"}
+
+
 def _cpu_worker(wid: int, nfr: int, cfg: dict, start, q):
     """One camera stream on one core: the oracle port of the reference chain
     frame by frame, single-threaded, as main_preview.py:94-109 runs it: C
@@ -697,9 +726,11 @@ def _cpu_baseline_leg(args, rank: int, world: int, cfg) -> dict:
     keeps its baseline too.  {} when disabled or not rank 0."""
     if rank != 0 or args.no_cpu_baseline or args.cpu_frames <= 0:
         return {}
-    workers = args.cpu_workers or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or \
-        len(os.sched_getaffinity(0))
-    return {"cpu_baseline": cpu_baseline(cfg, args.cpu_frames, workers)}
+    budget = host_cpu_budget()
+    workers = args.cpu_workers or budget["cpus"]
+    res = cpu_baseline(cfg, args.cpu_frames, workers)
+    res.update({"cpu_quota_cpus": budget["quota_cpus"], "cores_reason": budget["reason"]})
+    return {"cpu_baseline": res}
 
 
 def _rank_fields(t: dict, world: int, device) -> dict:

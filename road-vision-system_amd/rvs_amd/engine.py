@@ -11,6 +11,7 @@ step.  ``results()`` converts one step's device outputs into the reference's
 """
 from __future__ import annotations
 
+import warnings
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -72,17 +73,28 @@ class RoadVisionEngine:
                 self.detector.set_head_streams(False)
         self.max_det = self.detector.max_det if self.detector is not None else \
             int(det_cfg.get("max_det", 100))
+        # main_preview.py:64-78: a tracker or projector that fails to build
+        # is reported and left off (the run goes on without that feature)
         if projector is None:
             geom = cfg.get("geometry", {}) or {}
             if geom.get("enabled", False):
-                projector = build_projector(geom)
+                try:
+                    projector = build_projector(geom)
+                except Exception as exc:
+                    warnings.warn(f"geometry projector init failed, running without it: {exc}")
+                    projector = None
         self.projector = projector
         self.tracker = None
         if self.tracking_enabled and self.detector is not None:
-            self.tracker = MultiStreamSort(trk_cfg, self.S, tmax=tmax, dmax=self.max_det,
-                                           device=self.device)
-            self.tracker.set_projector(projector)
-        elif self.detector is not None:
+            try:
+                tracker = MultiStreamSort(trk_cfg, self.S, tmax=tmax, dmax=self.max_det,
+                                          device=self.device)
+                tracker.set_projector(projector)
+                self.tracker = tracker
+            except Exception as exc:
+                warnings.warn(f"tracker init failed, running without it: {exc}")
+                self.tracker = None
+        if self.tracker is None and self.detector is not None:
             # tracker off (main_preview.py:104-109): ids and speeds stay None,
             # each detection gets projector.distance_for_bbox when a projector exists
             self._untracked = _UntrackedMetrics(self.S, self.max_det, projector, self.device)
@@ -94,6 +106,11 @@ class RoadVisionEngine:
         # default chain: CLAHE + median + the detector's LetterBox in one pass
         self.fused_letterbox = self.detector is not None and \
             self.pipeline.letterbox_fusable(self.H, self.W, self.detector.geo)
+
+    def _need_detector(self, what: str) -> None:
+        if self.detector is None:
+            raise ValueError(f"{what} needs the detector (detect.enabled is false); "
+                             "step() runs the preprocess-only path")
 
     def preprocess_stage(self, frames: torch.Tensor, lb_slot: int = 0, lb_off: int = 0):
         """pipeline(raw) + the detector's LetterBox (main_preview.py:94-99)
@@ -129,10 +146,12 @@ class RoadVisionEngine:
         land in candidate slot `slot`.  part 1 / 2: the two halves of the
         forward (YoloEngine.forward_raw); part 2 continues part 1's batch
         (`batch` images, default S * pair)."""
+        self._need_detector("yolo_stage")
         self.detector.forward_raw(lb, slot=slot, lane=lane, part=part,
                                   batch=batch if batch is not None else self.S * self.pair)
 
     def detect_stage(self, frames: torch.Tensor, slot: int = 0) -> torch.Tensor:
+        self._need_detector("detect_stage")
         proc, lb = self.preprocess_stage(frames)
         self.yolo_stage(lb, slot)
         return proc
@@ -141,6 +160,7 @@ class RoadVisionEngine:
         """Autotune the detector's conv kernels on one batch of these frames
         (YoloEngine.autotune; pair mode: the batch of P*S the pipelined
         forwards run, the frames repeated); call outside graph capture."""
+        self._need_detector("autotune")
         for h in range(self.pair):
             self.preprocess_stage(frames, 0, h * self.S)
         lb = self.detector.lb[0][:self.S * self.pair]
@@ -150,6 +170,7 @@ class RoadVisionEngine:
                     record: Optional[Record] = None) -> Dict[str, torch.Tensor]:
         """NMS of candidate slot `slot` + SORT/geometry (main_preview.py:99-109),
         then the hand-back of the results into `record` (pinned host)."""
+        self._need_detector("track_stage")
         dets, det_n = self.detector.nms(ts.shape[0], slot)
         tid, dist, spd = self._metrics(dets, det_n, ts)
         out = {"dets": dets, "det_n": det_n, "track_id": tid, "distance_m": dist,
@@ -165,6 +186,7 @@ class RoadVisionEngine:
         """Pair mode: NMS of the P*S images of candidate slot `slot` at once,
         then SORT + hand-back of each of the P steps in order (step h owns
         images [h*S, (h+1)*S))."""
+        self._need_detector("track_pair_stage")
         S = self.S
         dets, det_n = self.detector.nms(S * len(ts_list), slot)
         outs = []
@@ -180,6 +202,7 @@ class RoadVisionEngine:
         """SORT + geometry of one step's NMS output (S images), then its
         hand-back into `record` (tracker.update + the .cpu() hand-over of
         main_preview.py:99-109)."""
+        self._need_detector("track_handback")
         tid, dist, spd = self._metrics(dets, det_n, ts)
         handback(dets, det_n, tid, dist, spd, self.rec_stage, record.host)
 
@@ -196,6 +219,7 @@ class RoadVisionEngine:
         P consecutive steps into one letterbox slot, ONE forward over their
         P*S frames, then NMS + per-step SORT + hand-back (the work of one
         pipeline unit of schedule.PipelinedRun, each launch alone)."""
+        self._need_detector("step_unit")
         S = self.S
         procs = [self.preprocess_stage(f, 0, h * S)[0] for h, f in enumerate(frames_list)]
         self.yolo_stage(self.detector.lb[0][:S * len(frames_list)], 0)

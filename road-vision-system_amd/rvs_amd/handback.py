@@ -43,7 +43,10 @@ class Record:
     def __init__(self, S: int, dmax: int, device, host: bool = True):
         self.S, self.dmax = int(S), int(dmax)
         self.nbytes = record_bytes(self.S, self.dmax)
-        self.host = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True) if host else None
+        # pinned (the stream's D2H copy lands in it asynchronously) when the
+        # engine lives on a GPU; a CPU-device engine (host-logic tests) gets pageable memory
+        pin = torch.device(device).type == "cuda"
+        self.host = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=pin) if host else None
         self.seq = 0  # hand-backs issued into this record (RoadVisionEngine.results checks it)
 
     def detections(self, names: Sequence[str], pool: "DetectionPool" = None) -> List[List[Detection]]:

@@ -423,3 +423,30 @@ def test_detection_disabled_returns_empty_lists(cuda):
     with pytest.raises(ValueError):
         PipelinedRun(eng, [frames[0]], [torch.zeros(S, dtype=torch.float64, device=cuda)])
     eng.close()
+
+
+def test_projector_build_failure_runs_without_geometry(cuda):
+    """geometry.enabled with only 2 image points: the projector fails to
+    build, the engine warns and runs on without it (main_preview.py:72-78),
+    so SORT still assigns ids and every distance / speed stays None."""
+    from rvs_amd.engine import RoadVisionEngine
+    from rvs_amd.synth import road_frames
+    cfg = _cfg()
+    cfg["geometry"]["projector"]["image_points"] = IMG[:2]
+    cfg["geometry"]["projector"]["world_points"] = WLD[:2]
+    S, H, W = 2, 1080, 1920
+    with pytest.warns(UserWarning, match="projector"):
+        eng = RoadVisionEngine(cfg, S, (H, W), device=cuda)
+    assert eng.projector is None and eng.tracker is not None
+    frames = road_frames(S, 2, H, W, device=cuda)
+    n = 0
+    for f in range(2):
+        res = eng.results(eng.step(frames[f], torch.full((S,), f / 30.0, dtype=torch.float64,
+                                                         device=cuda)))
+        for s in res:
+            for d in s:
+                assert d.track_id is not None
+                assert d.distance_m is None and d.speed_kmh is None
+                n += 1
+    assert n > 0
+    eng.close()
