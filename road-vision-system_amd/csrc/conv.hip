@@ -333,6 +333,7 @@ struct PatchGeo {
   int tiles_x, tiles_y;
   int p_bytes;     // pinst * 1024
   int fast;        // epilogue_fast applies (epi_fast)
+  int stagger;     // 8-wave form: waves 4-7 run each tile's epilogue one step late
 };
 
 // The common epilogue (one bf16 output view, no upsampled copy, optional
@@ -454,7 +455,9 @@ __device__ __forceinline__ void epi_pack(const ConvArgs& a, f32x4 (&acc)[MR][NR]
       const uint32_t vr = (__umul24(opx[n], (uint32_t)a.res_cs) + a.res_co + cq) * 2;
 #pragma unroll
       for (int m = 0; m < MR; ++m) {
-        const uint32_t roff = cout0 + m * 16 < a.Cout ? vr + m * 32 : kDrop;
+        // invalid pixels (past the map's end on the last image's bottom
+        // tile row) and fragments beyond Cout read the dropped offset
+        const uint32_t roff = pv[n] && cout0 + m * 16 < a.Cout ? vr + m * 32 : kDrop;
         rq[m][n] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)roff, 0, 0));
       }
     }
@@ -1047,6 +1050,69 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
 #endif
   int ti = walk.t0;  // tile of the current step
   int grp = 0;       // chunk group of the current step
+  // Stagger (8-wave form): the two waves of a SIMD are wave w and w + 4 of
+  // this block, and with one barrier per step they reach their MFMAs and
+  // their epilogue VALU together.  Waves 4-7 ("late") instead finish each
+  // tile at the start of the NEXT step, right after the barrier, with the
+  // sums still in their accumulators: on every SIMD one wave's epilogue
+  // (bias, SiLU, pack, stores) then runs beside its partner's MFMAs
+  // (MI355X_MICROARCH.md "Two waves per SIMD" item 9).  Same values, same
+  // stores: outputs are bit-identical.
+  // (not built for the 5x2 / 2x4 tiles: their extra epilogue site spills)
+  constexpr bool kStagger = NW == 8 && !(MR == 5 && NR == 2) && !(MR == 2 && NR == 4);
+  const bool late = kStagger && g.stagger && wave >= 4;  // wave is a scalar
+  bool pend = false;  // late waves: a finished tile (ptile) awaits its epilogue
+  int ptile = 0;
+  constexpr bool kDefer = !F8 && MR * NR <= 10;
+  // epilogue of tile `tile` from acc; `pk`: pack only (stores after the
+  // barrier, epi_store)
+  auto finish = [&](int tile, EpiPend<MR, NR>& ep, bool pk) {
+    const int b = tile / tiles_img;
+    const int r = tile - b * tiles_img;
+    const int ty = r / g.tiles_x, tx = r - (r / g.tiles_x) * g.tiles_x;
+    bool pv[NR];
+    int pb[NR], py[NR], px[NR];
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      pb[n] = b;
+      py[n] = ty * g.R + orow[n];
+      px[n] = tx * g.C + ocol[n];
+      pv[n] = oin[n] && py[n] < a.Ho && px[n] < a.Wo;
+    }
+#ifdef RV_EPI_SKIP
+    if (a.Cout == 12345) {  // timing experiment: keep the MFMAs live, skip the epilogue
+      float t = 0.f;
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int n = 0; n < NR; ++n) t += acc[m][n][0] + acc[m][n][3];
+      ((float*)a.out0)[tid] = t;
+    }
+    if (true) {
+    } else
+#endif
+    if constexpr (F8) {
+      epilogue8<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias, dq);
+    } else if (g.fast) {
+      uint32_t opx[NR];
+#pragma unroll
+      for (int n = 0; n < NR; ++n) opx[n] = (uint32_t)((b * a.Ho + py[n]) * a.Wo + px[n]);
+      f32x4 bl[MR];
+      bias_tile(bl);
+      if constexpr (kDefer) {
+        if (pk)
+          epi_pack<MR, NR>(a, acc, cout0, pv, opx, quad, bl, ep);
+        else
+          epilogue_fast<MR, NR>(a, acc, cout0, pv, opx, quad, bl);
+      } else {
+        epilogue_fast<MR, NR>(a, acc, cout0, pv, opx, quad, bl);
+      }
+    } else {
+      f32x4 bl[MR];
+      bias_tile(bl);
+      epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bl);
+    }
+  };
   if constexpr (RESW)
     for (int c = 0; c < nch; ++c) dma_weights(c, smem + c * W_BYTES);
   prep_tile(ti);
@@ -1054,6 +1120,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
   __syncthreads();
   RV_PH(0);
   for (int s = 0; s < nsteps; ++s) {
+    EpiPend<MR, NR> ep;
+    if (kStagger && pend) {  // late waves: the previous tile, before its accumulators are reset
+      finish(ptile, ep, false);
+      pend = false;
+    }
     if (grp == 0) {
 #pragma unroll
       for (int m = 0; m < MR; ++m)
@@ -1071,49 +1142,12 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
     RV_PH(2);
     // a finished tile's packed outputs, stored after the barrier (tiles whose
     // pack registers fit beside the compute registers without spills)
-    constexpr bool kDefer = !F8 && MR * NR <= 10;
-    EpiPend<MR, NR> ep;
     if (last) {
-      const int b = ti / tiles_img;
-      const int r = ti - b * tiles_img;
-      const int ty = r / g.tiles_x, tx = r - (r / g.tiles_x) * g.tiles_x;
-      bool pv[NR];
-      int pb[NR], py[NR], px[NR];
-#pragma unroll
-      for (int n = 0; n < NR; ++n) {
-        pb[n] = b;
-        py[n] = ty * g.R + orow[n];
-        px[n] = tx * g.C + ocol[n];
-        pv[n] = oin[n] && py[n] < a.Ho && px[n] < a.Wo;
-      }
-#ifdef RV_EPI_SKIP
-      if (a.Cout == 12345) {  // timing experiment: keep the MFMAs live, skip the epilogue
-        float t = 0.f;
-#pragma unroll
-        for (int m = 0; m < MR; ++m)
-#pragma unroll
-          for (int n = 0; n < NR; ++n) t += acc[m][n][0] + acc[m][n][3];
-        ((float*)a.out0)[tid] = t;
-      }
-      if (true) {
-      } else
-#endif
-      if constexpr (F8) {
-        epilogue8<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias, dq);
-      } else if (g.fast) {
-        uint32_t opx[NR];
-#pragma unroll
-        for (int n = 0; n < NR; ++n) opx[n] = (uint32_t)((b * a.Ho + py[n]) * a.Wo + px[n]);
-        f32x4 bl[MR];
-        bias_tile(bl);
-        if constexpr (kDefer)
-          epi_pack<MR, NR>(a, acc, cout0, pv, opx, quad, bl, ep);
-        else
-          epilogue_fast<MR, NR>(a, acc, cout0, pv, opx, quad, bl);
+      if (late) {
+        pend = true;
+        ptile = ti;
       } else {
-        f32x4 bl[MR];
-        bias_tile(bl);
-        epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bl);
+        finish(ti, ep, true);
       }
       ti += walk.step;
       grp = 0;
@@ -1123,9 +1157,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
     }
     __syncthreads();
     if constexpr (kDefer) {
-      if (last && g.fast) epi_store<MR, NR>(a, ep);  // the finished tile's stores (epi_pack)
+      if (last && g.fast && !late) epi_store<MR, NR>(a, ep);  // the finished tile's stores (epi_pack)
     }
     RV_PH(4);
+  }
+  if (kStagger && pend) {
+    EpiPend<MR, NR> ep;
+    finish(ptile, ep, false);
   }
 #ifdef RV_PHASE_PROF
   if (lane == 0) {
@@ -1336,6 +1374,8 @@ static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& 
   const int nch = conv_nch(a);
   g.G = std::max(1, std::min(c.G, nch));
   g.fast = epi_fast(a) ? 1 : 0;
+  static const int stagger = getenv("RV_STAGGER") ? atoi(getenv("RV_STAGGER")) : 1;  // A/B switch
+  g.stagger = stagger;
   // per-lane offset registers of the kernel (patch_maxit)
   const int maxit = (a.stride == 2 ? 6 : 2) * NR + 2;
   if (ceil_div(g.pinst, NW) > maxit) return false;

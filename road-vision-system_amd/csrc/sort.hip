@@ -20,6 +20,7 @@
 // single lane scans.  If more than kKeyCap pairs qualify (e.g. thr <= 0) the
 // kernel falls back to the literal argmax loop over the IoU matrix in HBM.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #include <vector>
 #include "common.h"
@@ -80,21 +81,25 @@ __device__ __forceinline__ float4 x_to_bbox(const double* x) {
                      (float)(cy + 0.5 * h));
 }
 
-// _update_motion_matrix(dt) + kf.predict()
+// _update_motion_matrix(dt) + kf.predict(), in place row by row (few live
+// registers): row i of F P F^T needs P rows i and i + 4 (i < 3) or row i
+// alone, and rows 4..6 are read (for rows 0..2) before they are rewritten.
+// Same expressions, same rounding as the whole-matrix form.
 __device__ void kf_predict(Track& t, double dt_raw) {
   const double dt = fmax(1e-3, dt_raw);
-  double x[7];
-  for (int i = 0; i < 7; ++i) x[i] = t.x[i];
   // x = F x
-  t.x[0] = x[0] + dt * x[4];
-  t.x[1] = x[1] + dt * x[5];
-  t.x[2] = x[2] + dt * x[6];
+  t.x[0] = t.x[0] + dt * t.x[4];
+  t.x[1] = t.x[1] + dt * t.x[5];
+  t.x[2] = t.x[2] + dt * t.x[6];
   // P = F P F^T + Q, F = I + dt E (E: (0,4),(1,5),(2,6))
-  double FP[49];
-  for (int i = 0; i < 7; ++i)
-    for (int j = 0; j < 7; ++j) FP[i * 7 + j] = t.P[i * 7 + j] + (i < 3 ? dt * t.P[(i + 4) * 7 + j] : 0.0);
-  for (int i = 0; i < 7; ++i)
-    for (int j = 0; j < 7; ++j) t.P[i * 7 + j] = FP[i * 7 + j] + (j < 3 ? dt * FP[i * 7 + j + 4] : 0.0);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    double f[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) f[j] = t.P[i * 7 + j] + (i < 3 ? dt * t.P[(i + 4) * 7 + j] : 0.0);
+#pragma unroll
+    for (int j = 0; j < 7; ++j) t.P[i * 7 + j] = f[j] + (j < 3 ? dt * f[j + 4] : 0.0);
+  }
   const double q0 = 0.04 * dt * dt;
   t.P[0] += q0;
   t.P[8] += q0;
@@ -149,43 +154,75 @@ __device__ void inv4(const double* S, double* Si) {
     for (int j = 0; j < 4; ++j) Si[i * 4 + j] = a[i][j + 4];
 }
 
-// kf.update(z) with R = diag(1, 1, 10, 10), H = [I4 0] (Joseph form)
-__device__ void kf_update(Track& t, const double z[4]) {
+// kf.update(z) with R = diag(1, 1, 10, 10), H = [I4 0] (Joseph form), on a
+// per-lane LDS scratch `sc` (kKfScratch doubles, element e at
+// sc[e * stride]): a copy of P, K = P H^T S^-1, then AP = A P and finally
+// P = AP A^T + K R K^T written over the track's P.  A = I - K H is formed
+// entry by entry from K (never stored).  The outer loops stay rolled over
+// LDS-resident operands, so the live set is one row (the whole-matrix
+// form held A, AP, K and P at once: 330 VGPRs, one wave per SIMD, and it
+// could not share a workgroup with the association).  Every sum keeps its
+// k order: bit-identical to the whole-matrix form.
+constexpr int kKfP = 0, kKfAP = 49, kKfK = 98, kKfScratch = 126;
+__device__ void kf_update(Track& t, const double z[4], double* sc, int stride) {
   const double R[4] = {1.0, 1.0, 10.0, 10.0};
-  double y[4], S[16], Si[16], K[28];
-  for (int i = 0; i < 4; ++i) y[i] = z[i] - t.x[i];
-  for (int i = 0; i < 4; ++i)
-    for (int j = 0; j < 4; ++j) S[i * 4 + j] = t.P[i * 7 + j] + (i == j ? R[i] : 0.0);
-  inv4(S, Si);
-  for (int i = 0; i < 7; ++i)
-    for (int j = 0; j < 4; ++j) {
-      double acc = 0.0;
-      for (int k = 0; k < 4; ++k) acc += t.P[i * 7 + k] * Si[k * 4 + j];
-      K[i * 4 + j] = acc;
-    }
+#define KF_P(i, j) sc[(kKfP + (i) * 7 + (j)) * stride]
+#define KF_AP(i, j) sc[(kKfAP + (i) * 7 + (j)) * stride]
+#define KF_K(i, j) sc[(kKfK + (i) * 4 + (j)) * stride]
+#define KF_A(i, k) (((i) == (k) ? 1.0 : 0.0) - ((k) < 4 ? KF_K(i, k) : 0.0))
+  for (int e = 0; e < 49; ++e) sc[(kKfP + e) * stride] = t.P[e];
+  double y[4];
+  {
+    double S[16], Si[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y[i] = z[i] - t.x[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) S[i * 4 + j] = KF_P(i, j) + (i == j ? R[i] : 0.0);
+    inv4(S, Si);
+#pragma unroll 1
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc += KF_P(i, k) * Si[k * 4 + j];
+        KF_K(i, j) = acc;
+      }
+  }
+#pragma unroll 1
   for (int i = 0; i < 7; ++i) {
     double acc = 0.0;
-    for (int k = 0; k < 4; ++k) acc += K[i * 4 + k] * y[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc += KF_K(i, k) * y[k];
     t.x[i] += acc;
   }
-  // A = I - K H (7x7; only the first 4 columns of KH are non-zero)
-  double A[49], AP[49];
+#pragma unroll 1
   for (int i = 0; i < 7; ++i)
-    for (int j = 0; j < 7; ++j) A[i * 7 + j] = (i == j ? 1.0 : 0.0) - (j < 4 ? K[i * 4 + j] : 0.0);
-  for (int i = 0; i < 7; ++i)
+#pragma unroll
     for (int j = 0; j < 7; ++j) {
       double acc = 0.0;
-      for (int k = 0; k < 7; ++k) acc += A[i * 7 + k] * t.P[k * 7 + j];
-      AP[i * 7 + j] = acc;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) acc += KF_A(i, k) * KF_P(k, j);
+      KF_AP(i, j) = acc;
     }
+#pragma unroll 1
   for (int i = 0; i < 7; ++i)
+#pragma unroll
     for (int j = 0; j < 7; ++j) {
       double acc = 0.0;
-      for (int k = 0; k < 7; ++k) acc += AP[i * 7 + k] * A[j * 7 + k];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) acc += KF_AP(i, k) * KF_A(j, k);
       double krk = 0.0;
-      for (int k = 0; k < 4; ++k) krk += K[i * 4 + k] * R[k] * K[j * 4 + k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) krk += KF_K(i, k) * R[k] * KF_K(j, k);
       t.P[i * 7 + j] = acc + krk;
     }
+#undef KF_P
+#undef KF_AP
+#undef KF_K
+#undef KF_A
 }
 
 // HomographyProjector.project_point / GroundProjector.distance (track_math.h)
@@ -279,6 +316,25 @@ __device__ void track_init(Track& t, int id, const float* det, double ts) {
 #define RV_ASSOC_THREADS 1024
 #endif
 constexpr int kAssocThreads = RV_ASSOC_THREADS;
+#ifndef RV_SORT_FUSED_THREADS
+#define RV_SORT_FUSED_THREADS 512
+#endif
+
+// Association workgroup LDS: tbox (tmax float4), dbox (dmax float4), keys
+// (kKeyCap u64), tupd (tmax f64), det_match (dmax), trk_match / ord / rank_t
+// / frank (tmax int each), rank_d / newslot (dmax int each), used (tmax u8);
+// the fused form adds the KF update scratch (kUpd x 126 f64, from offset 0)
+// and the detection jobs (dmax int2) at sort_ljob_off.
+constexpr int kUpdLanes = 64;
+__host__ __device__ inline size_t sort_assoc_bytes(int tmax, int dmax) {
+  return (size_t)(tmax + dmax) * 16 + (size_t)kKeyCap * 8 + (size_t)tmax * 8 + (size_t)dmax * 4 * 3 +
+         (size_t)tmax * 4 * 4 + (size_t)tmax;
+}
+__host__ __device__ inline size_t sort_ljob_off(int tmax, int dmax, int kupd) {
+  const size_t a = (sort_assoc_bytes(tmax, dmax) + 15) & ~(size_t)15;
+  const size_t b = (size_t)kupd * 126 * 8;  // kKfScratch doubles per update lane
+  return a > b ? a : b;
+}
 
 struct SortWs {  // per-frame workspace views (rv_sort_ws_bytes)
   float* M;         // S x tmax x dmax IoU matrix (argmax fallback only)
@@ -306,18 +362,18 @@ __global__ __launch_bounds__(256) void sort_predict_kernel(const StreamHdr* __re
 // Exclusive prefix of flag(i) over [0, n) for a kAssocThreads block,
 // chunked: out[i] = rank of i among the flagged, -1 if not flagged; returns
 // the total.  `wtot`: kAssocThreads / 64 ints of LDS scratch.
-template <class F>
+template <int NT, class F>
 __device__ int block_rank(F flag, int n, int* out, int* wtot) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int base = 0;
-  for (int c0 = 0; c0 < n; c0 += kAssocThreads) {
+  for (int c0 = 0; c0 < n; c0 += NT) {
     const int i = c0 + tid;
     const bool f = i < n && flag(i);
     const unsigned long long m = __ballot(f);
     if (lane == 0) wtot[w] = __popcll(m);
     __syncthreads();
     int pre = base, tot = 0;
-    for (int k = 0; k < kAssocThreads / 64; ++k) {
+    for (int k = 0; k < NT / 64; ++k) {
       pre += k < w ? wtot[k] : 0;
       tot += wtot[k];
     }
@@ -332,7 +388,8 @@ __device__ int block_rank(F flag, int n, int* out, int* wtot) {
 __device__ __forceinline__ void sort_update_row(Track* __restrict__ pool, const float* __restrict__ dets,
                                                 double ts, int s, int d, int2 j, const SortParams& p,
                                                 int* __restrict__ out_id, double* __restrict__ out_dist,
-                                                double* __restrict__ out_speed) {
+                                                double* __restrict__ out_speed, double* ap,
+                                                int ap_stride) {
   const size_t o = (size_t)s * p.dmax + d;
   out_id[o] = -1;
   out_dist[o] = NAN;
@@ -347,7 +404,7 @@ __device__ __forceinline__ void sort_update_row(Track* __restrict__ pool, const 
   if (j.y < 0) {  // matched: _Track.update + update_metrics
     double z[4];
     bbox_to_z(de[0], de[1], de[2], de[3], z);
-    kf_update(tr, z);
+    kf_update(tr, z, ap, ap_stride);
     tr.t_pred = ts;
     tr.t_upd = ts;
     tr.hits += 1;
@@ -365,11 +422,24 @@ __device__ __forceinline__ void sort_update_row(Track* __restrict__ pool, const 
   }
 }
 
-__global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
+// FUSED (rv_sort_update's default, one launch per frame): the block also
+// runs the KF predict of its stream's tracks (sort_predict_kernel's work,
+// boxes and last_update_ts straight into LDS) and, after the bookkeeping,
+// the per-detection updates (sort_update_kernel's work, jobs from LDS), so
+// a frame is one launch of S workgroups instead of three dependent ones --
+// fewer queue waits beside the persistent conv grids and no HBM round trip
+// of the predicted boxes and jobs.  A workgroup of NT = 256 threads gives
+// the update's f64 Kalman algebra the whole register file (one wave per
+// SIMD) without spills.
+template <int NT, bool FUSED>
+__global__ __launch_bounds__(NT) void sort_associate_kernel(
     StreamHdr* __restrict__ hdr, int* __restrict__ order, Track* __restrict__ pool,
     const float* __restrict__ dets, const int* __restrict__ dcount,
-    const double* __restrict__ ts_arr, SortParams p, SortWs ws) {
+    const double* __restrict__ ts_arr, SortParams p, SortWs ws, int* __restrict__ out_id,
+    double* __restrict__ out_dist, double* __restrict__ out_speed) {
+  constexpr int kAssocThreads = NT;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int kUpd = NT < kUpdLanes ? NT : kUpdLanes;  // FUSED: threads running the KF updates
   float4* tbox = (float4*)smem;                     // tmax
   float4* dbox = tbox + p.tmax;                     // dmax
   uint64_t* keys = (uint64_t*)(dbox + p.dmax);      // kKeyCap
@@ -382,6 +452,10 @@ __global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
   int* rank_d = frank + p.tmax;                     // dmax: new-track rank
   int* newslot = rank_d + p.dmax;                   // dmax: slot of the r-th new track
   uint8_t* used = (uint8_t*)(newslot + p.dmax);     // tmax
+  // FUSED: the detection jobs, after `used` and after the KF update
+  // scratch (kUpd x 126 doubles, which reuses the dead association arrays
+  // from offset 0 once the bookkeeping is done)
+  int2* ljob = (int2*)(smem + sort_ljob_off(p.tmax, p.dmax, kUpd));
   __shared__ int s_cnt, s_red_v[16], s_red_i[16], wtot[16];
 
   const int s = blockIdx.x;
@@ -397,9 +471,18 @@ __global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
   Track* pl = pool + (size_t)s * p.tmax;
 
   for (int t = tid; t < T; t += kAssocThreads) {
-    tbox[t] = ws.tbox[(size_t)s * p.tmax + t];
-    tupd[t] = ws.tupd[(size_t)s * p.tmax + t];
-    ord[t] = ord_g[t];
+    const int slot = ord_g[t];
+    if constexpr (FUSED) {  // sort_predict_kernel's work for list index t
+      Track& tr = pl[slot];
+      kf_predict(tr, ts - tr.t_pred);
+      tr.t_pred = ts;
+      tbox[t] = x_to_bbox(tr.x);
+      tupd[t] = tr.t_upd;
+    } else {
+      tbox[t] = ws.tbox[(size_t)s * p.tmax + t];
+      tupd[t] = ws.tupd[(size_t)s * p.tmax + t];
+    }
+    ord[t] = slot;
     trk_match[t] = -1;
   }
   for (int d = tid; d < D; d += kAssocThreads) {
@@ -554,8 +637,8 @@ __global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
   __syncthreads();
 
   // ---- bookkeeping (sort_tracker.py:234-276)
-  const int n_new = block_rank([&](int d) { return det_match[d] < 0; }, D, rank_d, wtot);
-  const int n_surv = block_rank(
+  const int n_new = block_rank<NT>([&](int d) { return det_match[d] < 0; }, D, rank_d, wtot);
+  const int n_surv = block_rank<NT>(
       [&](int t) {
         const double upd = trk_match[t] >= 0 ? ts : tupd[t];
         return (ts - upd) <= p.max_staleness;
@@ -578,7 +661,7 @@ __global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
   const bool new_alive = 0.0 <= p.max_staleness;
   const int room = p.tmax - n_surv;
   const int n_fit = !new_alive ? 0 : (n_new < room ? n_new : room);
-  block_rank([&](int q) { return !used[q]; }, p.tmax, frank, wtot);
+  block_rank<NT>([&](int q) { return !used[q]; }, p.tmax, frank, wtot);
   for (int q = tid; q < p.tmax; q += kAssocThreads) {
     const int r = frank[q];
     if (r >= 0 && r < n_fit) newslot[r] = q;
@@ -599,7 +682,10 @@ __global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
         j = make_int2(r < n_fit ? newslot[r] : -1, h.next_id + r);
       }
     }
-    job[d] = j;
+    if constexpr (FUSED)
+      ljob[d] = j;
+    else
+      job[d] = j;
   }
   if (tid == 0) {
     StreamHdr o;
@@ -609,18 +695,28 @@ __global__ __launch_bounds__(kAssocThreads) void sort_associate_kernel(
     o.pad = 0;
     hdr[s] = o;
   }
+  if constexpr (FUSED) {
+    // sort_update_kernel's work: the streak resets above and the predicted
+    // states are this block's own global writes, visible after the barrier
+    __syncthreads();
+    double* ap = (double*)smem + tid;
+    if (tid < kUpd)
+      for (int d = tid; d < p.dmax; d += kUpd)
+        sort_update_row(pool, dets, ts, s, d, ljob[d], p, out_id, out_dist, out_speed, ap, kUpd);
+  }
 }
 
 // One thread per detection row of every stream (sort_tracker.py:234-269).
-__global__ __launch_bounds__(256) void sort_update_kernel(
+__global__ __launch_bounds__(kUpdLanes) void sort_update_kernel(
     Track* __restrict__ pool, const float* __restrict__ dets, const double* __restrict__ ts_arr,
     SortParams p, SortWs ws, int* __restrict__ out_id, double* __restrict__ out_dist,
     double* __restrict__ out_speed) {
+  __shared__ double ap[126 * kUpdLanes];  // KF update scratch (kKfScratch), element-major
   const int s = blockIdx.y;
-  const int d = blockIdx.x * 256 + threadIdx.x;
+  const int d = blockIdx.x * kUpdLanes + threadIdx.x;
   if (d >= p.dmax) return;
   sort_update_row(pool, dets, ts_arr[s], s, d, ws.det_job[(size_t)s * p.dmax + d], p, out_id,
-                  out_dist, out_speed);
+                  out_dist, out_speed, ap + threadIdx.x, kUpdLanes);
 }
 
 // Per-stream state layout: headers (S x 16 B, padded to 256 B), the list
@@ -703,9 +799,16 @@ extern "C" size_t rv_sort_ws_bytes(int S, int tmax, int dmax) {
   return ws_parts(S, tmax, dmax, off);
 }
 
-static size_t sort_smem(int tmax, int dmax) {
-  return (size_t)(tmax + dmax) * 16 + (size_t)kKeyCap * 8 + (size_t)tmax * 8 +
-         (size_t)dmax * 4 * 3 + (size_t)tmax * 4 * 4 + (size_t)tmax;
+constexpr int kFusedThreads = RV_SORT_FUSED_THREADS;
+static size_t sort_smem(int tmax, int dmax, bool fused) {
+  const int kupd = kFusedThreads < kUpdLanes ? kFusedThreads : kUpdLanes;
+  return fused ? sort_ljob_off(tmax, dmax, kupd) + (size_t)dmax * 8 : sort_assoc_bytes(tmax, dmax);
+}
+
+// RV_SORT_FUSED=0: the three-launch form (A/B)
+static bool sort_fused() {
+  static const int v = getenv("RV_SORT_FUSED") ? atoi(getenv("RV_SORT_FUSED")) : 1;
+  return v != 0;
 }
 
 extern "C" int rv_sort_init(void* state, int S, int tmax, void* stream) {
@@ -754,7 +857,8 @@ extern "C" int rv_sort_update(void* state_in, void* state_out, int S, int tmax,
     p.origin[0] = origin2[0];
     p.origin[1] = origin2[1];
   }
-  const size_t smem = sort_smem(tmax, dmax);
+  const bool fused = sort_fused();
+  const size_t smem = sort_smem(tmax, dmax, fused);
   RV_CHECK_ARG(smem <= 160 * 1024, "tmax/dmax need %zu B of LDS", smem);
   hipStream_t st = as_stream(stream);
   int r = RV_OK;
@@ -763,16 +867,17 @@ extern "C" int rv_sort_update(void* state_in, void* state_out, int S, int tmax,
                                  hipMemcpyDeviceToDevice, st),
                   "rv_sort_update state copy");
   if (r) return r;
-  static int attr_set = 0;
-  if ((int)smem > attr_set) {  // once per growth, outside steady-state launches
-    hipError_t e = hipFuncSetAttribute((const void*)sort_associate_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  static int attr_set[2] = {0, 0};
+  const void* assoc_fn = fused ? (const void*)sort_associate_kernel<kFusedThreads, true>
+                               : (const void*)sort_associate_kernel<kAssocThreads, false>;
+  if ((int)smem > attr_set[fused]) {  // once per growth, outside steady-state launches
+    hipError_t e = hipFuncSetAttribute(assoc_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) {
       set_error("hipFuncSetAttribute(%zu B LDS): %s", smem, hipGetErrorString(e));
       (void)hipGetLastError();
       return -(int)e;
     }
-    attr_set = (int)smem;
+    attr_set[fused] = (int)smem;
   }
   const StateView v = state_view(state_out, S, tmax);
   size_t off[4];
@@ -782,16 +887,21 @@ extern "C" int rv_sort_update(void* state_in, void* state_out, int S, int tmax,
   w.tbox = (float4*)((uint8_t*)ws + off[1]);
   w.tupd = (double*)((uint8_t*)ws + off[2]);
   w.det_job = (int2*)((uint8_t*)ws + off[3]);
+  if (fused) {
+    sort_associate_kernel<kFusedThreads, true><<<S, kFusedThreads, smem, st>>>(
+        v.hdr, v.order, v.pool, dets, dcount, ts, p, w, out_id, out_dist, out_speed);
+    return launch_status("rv_sort_update (fused)");
+  }
   sort_predict_kernel<<<dim3(ceil_div(tmax, 256), S), 256, 0, st>>>(v.hdr, v.order, v.pool, ts,
                                                                      tmax, w);
   r = launch_status("rv_sort_update (predict)");
   if (r) return r;
-  sort_associate_kernel<<<S, kAssocThreads, smem, st>>>(v.hdr, v.order, v.pool, dets, dcount, ts, p,
-                                                       w);
+  sort_associate_kernel<kAssocThreads, false><<<S, kAssocThreads, smem, st>>>(
+      v.hdr, v.order, v.pool, dets, dcount, ts, p, w, out_id, out_dist, out_speed);
   r = launch_status("rv_sort_update (associate)");
   if (r) return r;
-  sort_update_kernel<<<dim3(ceil_div(dmax, 256), S), 256, 0, st>>>(v.pool, dets, ts, p, w, out_id,
-                                                                   out_dist, out_speed);
+  sort_update_kernel<<<dim3(ceil_div(dmax, kUpdLanes), S), kUpdLanes, 0, st>>>(
+      v.pool, dets, ts, p, w, out_id, out_dist, out_speed);
   return launch_status("rv_sort_update (update)");
 }
 
