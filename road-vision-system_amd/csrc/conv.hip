@@ -320,9 +320,14 @@ static inline int xcd_grid(int want, int ntiles, bool persist) {
   return g >= 8 ? g & ~7 : g;
 }
 
+// cache-policy bits of the activation-patch DMA (A/B builds: 2 = nt)
+#ifndef RV_CONV_IN_AUX
+#define RV_CONV_IN_AUX 0
+#endif
+template <int AUX = 0>
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
-                                           (int)voff, soff, 0, 0);
+                                           (int)voff, soff, 0, AUX);
 }
 
 struct PatchGeo {
@@ -889,13 +894,29 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
       const int c = grp * G + gi;
       if (c >= nch) break;
       uint8_t* P = stages + buf * stage_bytes + gi * chunk_bytes;
-      const bool tail = has_tail && c == nch - 1;
+      const bool tail = has_tail && c == nch - 1;  // block-uniform
+      // Two paths: a select feeding every DMA (tail chunk only) made the
+      // compiler route all of them through ONE address VGPR, and each
+      // v_cndmask into it then waited for the previous buffer_load to read
+      // its operand (a VMEM-read / VALU-write interlock per DMA); the common
+      // path issues straight from the per-slot offset registers.
+#ifdef RV_DMA_SELECT_ALWAYS  // A/B: the r05 single path
+      if (true) {
+#else
+      if (tail) {
+#endif
 #pragma unroll
-      for (int it = 0; it < MAXP; ++it) {
-        const int j = wave + NW * it;
-        if (j < g.pinst) {
-          const uint32_t v = tail && ((tailbad >> it) & 1) ? kOOB : voff[it];
-          dma16(img_rsrc, P + j * 1024, v, c * 64);
+        for (int it = 0; it < MAXP; ++it) {
+          const int j = wave + NW * it;
+          if (j < g.pinst)
+            dma16<RV_CONV_IN_AUX>(img_rsrc, P + j * 1024,
+                                  tail && ((tailbad >> it) & 1) ? kOOB : voff[it], c * 64);
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < MAXP; ++it) {
+          const int j = wave + NW * it;
+          if (j < g.pinst) dma16<RV_CONV_IN_AUX>(img_rsrc, P + j * 1024, voff[it], c * 64);
         }
       }
       if constexpr (!RESW) dma_weights(c, P + g.p_bytes);
