@@ -179,6 +179,11 @@ int rv_yolo_destroy(void* handle);
  * caller whose stages already overlap).  The environment variable
  * RV_HEAD_STREAMS=0/1 overrides it. */
 #define RV_YOLO_OPT_HEAD_STREAMS 4
+/* RV_YOLO_OPT_FUSE_CV1 (default 1): model.3 and model.4.cv1 (the C2f's
+ * first 1x1) run as one launch -- the 1x1 works on model.3's output tile in
+ * LDS, so that map never reaches HBM; bit-identical to the two launches.
+ * Raw parity forwards with RV_YOLO_OPT_RAW_UNFUSED keep them separate. */
+#define RV_YOLO_OPT_FUSE_CV1 5
 int rv_yolo_set_option(void* handle, int opt, int value);
 
 /* fp8 plans (BASELINE configs[4]: "YOLOv8m 1280x1280 fp8 MFMA conv path").

@@ -58,6 +58,12 @@ struct ConvArgs {
   // full resolution).  split = 0 and in_up = 0: `in` only.
   const bf16_t* in2;
   int in2_cs, in2_co, split, in_up;
+  // chained 1x1 conv (conv_patch_kernel CH form): a C2f cv1 (Cout -> Cout,
+  // SiLU) fused into the conv producing its input.  ch_w: its packed
+  // weights [Cout][Cout] bf16, ch_b: its bias.  The launch's output view
+  // (out0) is then the 1x1's; the producer's own output stays in LDS.
+  const bf16_t* ch_w;
+  const float* ch_b;
 };
 
 // One configuration of the LDS-staged conv kernel: MR x NR 16x16 fragments

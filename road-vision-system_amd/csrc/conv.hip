@@ -219,6 +219,11 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
     return launch_conv_cfg(a, c, s);
   }
   if (try_launch_patch(a, s, &st)) return st;
+  if (a.ch_w) {
+    set_error("chained 1x1 conv (Cout %d, k%d s%d) has no patch-kernel configuration", a.Cout, a.k,
+              a.stride);
+    return RV_EINVAL;
+  }
   if (a.in8) {
     set_error("fp8 conv (Cin %d, Cout %d, k%d s%d) has no patch-kernel configuration", a.Cin,
               a.Cout, a.k, a.stride);
@@ -713,7 +718,10 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& a, f32x4 (&acc)[MR][NR
 // so a resident weight slab (or a staged chunk of weights) is shared by 8
 // waves and the pixel tile is twice as large -- half the LDS-DMA bytes per
 // MFMA of the 4-wave form at the same occupancy (2 waves per SIMD).
-template <int MR, int NR, int K, int S, bool RESW, bool F8, int NW = 4>
+// CH = true (ConvArgs::ch_w): a chained 1x1 conv Cout -> Cout (a C2f cv1
+// fused into the conv producing its input; bf16, one cout tile covering
+// Cout, MR even): see chain_tile below.
+template <int MR, int NR, int K, int S, bool RESW, bool F8, int NW = 4, bool CH = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(ConvArgs a, PatchGeo g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int T2 = K * K;
@@ -823,6 +831,26 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
 #pragma unroll
     for (int m = 0; m < MR; ++m) bl[m] = *(const f32x4*)(bias_lds + m * 16 + quad * 4);
   };
+  // CH: the chained 1x1's weights (chunk-major [c][row][64 B], the quarter
+  // swizzle of conv1x1_direct_kernel), its bias, and one x tile per wave
+  // (the wave's 16 NR pixels x Cout channels of the producer's bf16 output,
+  // chunk-major [c][pixel][64 B], quarter swizzle by pixel)
+  constexpr int CHN = MR / 2;                       // 32-channel chunks of the chained input
+  uint8_t* const ch_w_lds = (uint8_t*)(bias_lds + BC);
+  float* const ch_b_lds = (float*)(ch_w_lds + (CH ? CHN * BC * 64 : 0));
+  uint8_t* const ch_x_lds = (uint8_t*)(ch_b_lds + (CH ? BC : 0)) + wave * (CH ? CHN * NR * 16 * 64 : 0);
+  if constexpr (CH) {
+    static_assert(!F8 && MR % 2 == 0, "chained 1x1: bf16, whole 32-channel chunks");
+    // BC / 16 DMA instructions per chunk (16 rows x 64 B each)
+    for (int j = wave; j < CHN * (BC / 16); j += NW) {
+      const int c = j / (BC / 16), jr = j - c * (BC / 16);
+      const int row = jr * 16 + (lane >> 2);
+      const int q = (lane & 3) ^ swzq<false>(row);
+      __builtin_amdgcn_global_load_lds((const void*)(a.ch_w + (size_t)row * BC + c * 32 + q * 8),
+                                       (void*)(ch_w_lds + c * BC * 64 + jr * 1024), 16, 0, 0);
+    }
+    for (int i = tid; i < BC; i += 64 * NW) ch_b_lds[i] = a.ch_b[i];
+  }
   // Patch and weight DMA through buffer resources (buffer_load ... lds):
   // every DMA instruction's per-lane byte offset is computed once -- per
   // tile for the patch, per kernel for the weights --, the chunk offset
@@ -1084,9 +1112,78 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
   const bool late = kStagger && g.stagger && wave >= 4;  // wave is a scalar
   bool pend = false;  // late waves: a finished tile (ptile) awaits its epilogue
   int ptile = 0;
-  constexpr bool kDefer = !F8 && MR * NR <= 10;
+  constexpr bool kDefer = !F8 && !CH && MR * NR <= 10;
   // epilogue of tile `tile` from acc; `pk`: pack only (stores after the
   // barrier, epi_store)
+  // CH: the finished tile's producer values (bias, SiLU, bf16 -- what the
+  // unfused conv stores) go to this wave's x tile instead of HBM, then the
+  // chained 1x1 runs on them: per 32-channel chunk c ascending, A = its
+  // weights, B = the wave's pixels (the k order of conv1x1_direct_kernel and
+  // of the patch kernel's 1x1 form: bit-identical to the unfused launch),
+  // and its epilogue (bias, SiLU) stores the output views.  Each wave reads
+  // only the pixels it wrote (in-order LDS, no barrier).
+  auto chain_tile = [&](const bool (&pv)[NR], const uint32_t (&opx)[NR]) {
+    if constexpr (CH) {
+      f32x4 bl[MR];
+      bias_tile(bl);
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        const int px = n * 16 + col;
+#pragma unroll
+        for (int m = 0; m < MR; m += 2) {
+          uint32_t v0[2], v1[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = acc[m + h][n][i] + bl[m + h][i];
+            if (a.act) silu4(v);
+            v0[h] = pack_bf16x2(v[0], v[1]);
+            v1[h] = pack_bf16x2(v[2], v[3]);
+          }
+          // quad q: channels 16 (q & 1) + 8 (q >> 1) .. +7 of chunk m / 2
+          const auto x0 = __builtin_amdgcn_permlane16_swap(v0[0], v0[1], false, false);
+          const auto x1 = __builtin_amdgcn_permlane16_swap(v1[0], v1[1], false, false);
+          const int qq = 2 * (quad & 1) + (quad >> 1);
+          *(v4u32*)(ch_x_lds + ((m / 2) * NR * 16 + px) * 64 + ((qq ^ swzq<false>(px)) << 4)) =
+              v4u32{x0[0], x1[0], x0[1], x1[1]};
+        }
+      }
+      f32x4 acc2[MR][NR];
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int n = 0; n < NR; ++n) acc2[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < CHN; ++c) {
+        bf16x8 A2[MR], B2[NR];
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          const int row = m * 16 + col;
+          A2[m] = __builtin_bit_cast(
+              bf16x8, *(const uint4*)(ch_w_lds + c * BC * 64 + row * 64 + ((quad ^ swzq<false>(row)) << 4)));
+        }
+#pragma unroll
+        for (int n = 0; n < NR; ++n) {
+          const int px = n * 16 + col;
+          B2[n] = __builtin_bit_cast(
+              bf16x8, *(const uint4*)(ch_x_lds + (c * NR * 16 + px) * 64 + ((quad ^ swzq<false>(px)) << 4)));
+        }
+#pragma unroll
+        for (int m = 0; m < MR; ++m)
+#pragma unroll
+          for (int n = 0; n < NR; ++n)
+            acc2[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2[m], B2[n], acc2[m][n], 0, 0, 0);
+      }
+      f32x4 bl2[MR];
+#pragma unroll
+      for (int m = 0; m < MR; ++m) bl2[m] = *(const f32x4*)(ch_b_lds + m * 16 + quad * 4);
+      ConvArgs a2 = a;
+      a2.act = 1;
+      a2.res = nullptr;
+      epilogue_fast<MR, NR>(a2, acc2, 0, pv, opx, quad, bl2);
+    }
+  };
   auto finish = [&](int tile, EpiPend<MR, NR>& ep, bool pk) {
     const int b = tile / tiles_img;
     const int r = tile - b * tiles_img;
@@ -1114,6 +1211,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
 #endif
     if constexpr (F8) {
       epilogue8<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias, dq);
+    } else if constexpr (CH) {
+      uint32_t opx[NR];
+#pragma unroll
+      for (int n = 0; n < NR; ++n) opx[n] = (uint32_t)((b * a.Ho + py[n]) * a.Wo + px[n]);
+      chain_tile(pv, opx);
     } else if (g.fast) {
       uint32_t opx[NR];
 #pragma unroll
@@ -1404,6 +1506,8 @@ static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& 
   // two stages: the next (tile, chunk group) streams in during the current one
   smem = (c.resw ? nch * wb : 0) + 2 * (size_t)g.G * (g.p_bytes + (c.resw ? 0 : wb)) +
          (a.in8 ? 0 : (size_t)16 * MR * 4);  // bf16: the block's bias
+  if (a.ch_w)  // chained 1x1: its weights and bias, one x tile per wave
+    smem += (size_t)(MR / 2) * 16 * MR * 64 + (size_t)16 * MR * 4 + (size_t)NW * (MR / 2) * NR * 16 * 64;
   return smem <= 160 * 1024;
 }
 
@@ -1423,11 +1527,11 @@ static int num_cus() {
 
 // Every instantiation gets the full 160 KB dynamic-LDS cap once; resident
 // blocks per CU are cached per LDS size (per instantiation).
-template <int MR, int NR, int K, int S, bool RESW, bool F8 = false, int NW = 4>
+template <int MR, int NR, int K, int S, bool RESW, bool F8 = false, int NW = 4, bool CH = false>
 static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, int persist,
                           hipStream_t s) {
   static bool attr = false;
-  auto fn = conv_patch_kernel<MR, NR, K, S, RESW, F8, NW>;
+  auto fn = conv_patch_kernel<MR, NR, K, S, RESW, F8, NW, CH>;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        160 * 1024);
@@ -1542,9 +1646,28 @@ constexpr bool patch_spills8(int MR, int NR, int K, int S, bool RESW) {
                     (S == 2 && !RESW && MR == 1 && NR == 2));
 }
 
+// chained-1x1 (CH) instantiations: C2f cv1 behind a 64-channel 3x3 conv
+// (YOLOv8n model.3 -> model.4.cv1); ch_tile_ok is the host-side check
+template <int MR, int NR>
+constexpr bool ch_built() {
+  return MR == 4 && NR <= 2;
+}
+static bool ch_tile_ok(int mr, int nr) { return mr == 4 && nr <= 2; }
+template <int MR, int NR, bool RESW, int NW>
+static int launch_patch_ch(const ConvArgs& a, const PatchGeo& g, size_t smem, int persist,
+                           hipStream_t s) {
+  if constexpr (ch_built<MR, NR>()) {
+    if (a.k == 3 && a.stride == 2) return launch_patch_t<MR, NR, 3, 2, RESW, false, NW, true>(a, g, smem, persist, s);
+    if (a.k == 3 && a.stride == 1) return launch_patch_t<MR, NR, 3, 1, RESW, false, NW, true>(a, g, smem, persist, s);
+  }
+  set_error("conv_patch (chained 1x1): no variant MR=%d NR=%d k=%d s=%d", MR, NR, a.k, a.stride);
+  return RV_EINVAL;
+}
+
 template <int MR, int NR, bool RESW>
 static int launch_patch_ks(const ConvArgs& a, const PatchGeo& g, size_t smem, int persist,
                            hipStream_t s) {
+  if (a.ch_w) return launch_patch_ch<MR, NR, RESW, 4>(a, g, smem, persist, s);
   if (a.in8) {
     if constexpr (tile8_built<MR, NR>()) {
       if constexpr (!patch_spills(MR, NR, 3, 1, RESW) && !patch_spills8(MR, NR, 3, 1, RESW))
@@ -1581,6 +1704,7 @@ constexpr bool tile_w8_built() {
 template <int MR, int NR, bool RESW>
 static int launch_patch8_ks(const ConvArgs& a, const PatchGeo& g, size_t smem, int persist,
                             hipStream_t s) {
+  if (a.ch_w) return launch_patch_ch<MR, NR, RESW, 8>(a, g, smem, persist, s);
   if constexpr (tile_w8_built<MR, NR>()) {
     if (!a.in8 && a.k == 3 && a.stride == 1)
       return launch_patch_t<MR, NR, 3, 1, RESW, false, 8>(a, g, smem, persist, s);
@@ -1601,6 +1725,10 @@ static const int kTiles[][2] = {{8, 2}, {8, 1}, {5, 2}, {5, 1}, {4, 4}, {4, 2}, 
                                 {2, 4}, {2, 2}, {2, 1}, {1, 4}, {1, 2}, {1, 1}};
 
 bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c) {
+  if (a.ch_w &&  // chained 1x1: the patch kernel's CH form, one cout tile, fast epilogue
+      (c.kind == 1 || a.in8 || !ch_tile_ok(c.mr, c.nr) || 16 * c.mr != a.Cout || a.k != 3 ||
+       a.res || a.out1 || a.out0_up || !epi_fast(a) || a.g2_cout0 > 0 || vcat(a)))
+    return false;
   if (c.kind == 1) return !a.in8 && direct_ok(a, c);
   if ((c.kind != 0 && c.kind != 2) || vcat(a)) return false;
   if (c.kind == 2 && (a.in8 || a.k != 3 || !w8_tile(c.mr, c.nr))) return false;

@@ -344,6 +344,7 @@ struct Model {
   // RV_YOLO_OPT_STEM_X1: the fused stem also writes X1 (parity tests)
   int stem_x1 = 0;
   int head_streams = 1;            // RV_YOLO_OPT_HEAD_STREAMS
+  int fuse_cv1 = 1;                // RV_YOLO_OPT_FUSE_CV1
   std::vector<Buf> bufs;
   int nA = 0;
   int map_h[6], map_w[6];  // stride 2^i maps
@@ -560,7 +561,8 @@ struct Exec {
     auto ob = [&](int o8) { return a.out_f32 ? 4.0 : (o8 ? 1.0 : 2.0); };
     const double outs = (a.out0 ? (a.out0_up ? 4 : 1) * ob(a.out0_8) : 0) +
                         (a.out1 ? (a.out1_up ? 4 : 1) * ob(a.out1_8) : 0);
-    const double w = eb * a.k * a.k * ((double)cout1 * a.Cin + (double)cout2 * (g2 ? a.g2_Cin : 0));
+    const double w = eb * a.k * a.k * ((double)cout1 * a.Cin + (double)cout2 * (g2 ? a.g2_Cin : 0)) +
+                     (a.ch_w ? 2.0 * a.Cout * a.Cout : 0.0);  // a chained 1x1's weights
     return px_in * in_ch * eb + px_out * a.Cout * outs + (a.res ? px_out * a.Cout * eb : 0.0) + w;
   }
 
@@ -666,6 +668,35 @@ struct Exec {
     a.g2_bias = bptr(c2);
     a.g2_wscale = wsptr(c2);
     launch(a, i1, fl);
+  }
+
+  // conv n1 (3x3, output view `mid`, never written) with the 1x1 conv n2
+  // (Cout -> Cout, SiLU: a C2f cv1) chained inside the same launch
+  // (ConvArgs::ch_w, conv_patch_kernel CH form) writing view o0.  false
+  // when the pair does not have the chained form's shape (the caller then
+  // runs them as two launches).
+  bool conv_chain(const std::string& n1, View in, int li, View mid, const std::string& n2,
+                  View o0) {
+    if (status) return false;
+    const int i1 = M->def.find(n1), i2 = M->def.find(n2);
+    if (i1 < 0 || i2 < 0) return false;
+    const ConvSpec& c1 = M->def.convs[i1];
+    const ConvSpec& c2 = M->def.convs[i2];
+    if (c1.f8 || c2.f8 || c1.k != 3 || c1.cout != 64 || c2.k != 1 || c2.cin != c1.cout ||
+        c2.cout != c1.cout || !c1.act || !c2.act)
+      return false;
+    const View none{-1, 0, 0};
+    ConvArgs a = args(c1, in, li, o0, 0, none, 0, none);
+    ConvCfg probe{4, 1, 1, 1, 1, 0};
+    a.ch_w = wptr(c2);
+    a.ch_b = bptr(c2);
+    if (!conv_cfg_ok(a, probe)) return false;
+    // trace records: the two convs as the unfused plan runs them
+    trace(i1, args(c1, in, li, mid, 0, none, 0, none), in, mid, 0, none, 0, none);
+    const ConvArgs a2 = args(c2, mid, li + 1, o0, 0, none, 0, none);
+    trace(i2, a2, mid, o0, 0, none, 0, none);
+    launch(a, i1, flops_of(c1, a) + flops_of(c2, a2));
+    return true;
   }
 
   static bool c2f_will_fuse(int c, int n, bool fuse, int up0, View o1, View o0) {
@@ -949,6 +980,9 @@ extern "C" int rv_yolo_set_option(void* h, int opt, int value) {
     case RV_YOLO_OPT_HEAD_STREAMS:
       M->head_streams = value != 0;
       return RV_OK;
+    case RV_YOLO_OPT_FUSE_CV1:
+      M->fuse_cv1 = value != 0;
+      return RV_OK;
     default:
       set_error("unknown yolo option %d", opt);
       return RV_EINVAL;
@@ -1154,9 +1188,24 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
     return RV_OK;
   }
   }  // part != 4
-  E.conv("model.3", View{M->X2, v.c2, 0}, 2, View{M->X3, v.c3, 0});
-  E.c2f("model.4", View{M->X3, v.c3, 0}, 3, M->C4, v.c3, v.nm, true,
-        View{M->CAT14, cat14, v.h12}, 0, View{-1, 0, 0}, 0, v.c3 / 2 == 16 ? fuse_c2f : fuse_c2f32);
+  // model.3 + model.4.cv1 in one launch (the chained 1x1: model.3's output
+  // map is only ever read by model.4.cv1) unless a raw parity forward keeps
+  // every activation (RV_YOLO_OPT_RAW_UNFUSED), RV_YOLO_OPT_FUSE_CV1 = 0 or
+  // RV_FUSE_CV1=0
+  {
+    static const bool cv1_env = !getenv("RV_FUSE_CV1") || atoi(getenv("RV_FUSE_CV1")) != 0;
+    const bool f4 = v.c3 / 2 == 16 ? fuse_c2f : fuse_c2f32;
+    const int c4 = v.c3 / 2;
+    const int c4cs = E.c2f_will_fuse(c4, v.nm, f4, 0, View{-1, 0, 0}, View{M->CAT14, cat14, v.h12})
+                         ? 2 * c4
+                         : (2 + v.nm) * c4;
+    const bool chained = cv1_env && M->fuse_cv1 && !f8 && !(raw_out && M->raw_unfused) &&
+                         E.conv_chain("model.3", View{M->X2, v.c2, 0}, 2, View{M->X3, v.c3, 0},
+                                      "model.4.cv1", View{M->C4, c4cs, 0});
+    if (!chained) E.conv("model.3", View{M->X2, v.c2, 0}, 2, View{M->X3, v.c3, 0});
+    E.c2f("model.4", View{M->X3, v.c3, 0}, 3, M->C4, v.c3, v.nm, true,
+          View{M->CAT14, cat14, v.h12}, 0, View{-1, 0, 0}, 0, f4, chained);
+  }
   E.conv("model.5", View{M->CAT14, cat14, v.h12}, 3, View{M->X5, v.c4, 0});
   E.c2f("model.6", View{M->X5, v.c4, 0}, 4, M->C6, v.c4, v.nm, true,
         View{M->CAT11, cat11, v.c5});

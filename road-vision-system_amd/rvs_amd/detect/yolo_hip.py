@@ -212,6 +212,13 @@ class YoloEngine:
         for h in self._hs:
             call("rv_yolo_set_option", h, 4, 1 if on else 0)
 
+    def set_fuse_cv1(self, on: bool) -> None:
+        """model.3 and model.4.cv1 as one launch with the 1x1 chained on
+        model.3's output tile in LDS (True, default) or as two launches
+        (RV_YOLO_OPT_FUSE_CV1; bit-identical results)."""
+        for h in self._hs:
+            call("rv_yolo_set_option", h, 5, 1 if on else 0)
+
     def set_fuse_c2f(self, on) -> None:
         """Narrow C2f blocks as one fused launch or one launch per conv
         (RV_YOLO_OPT_FUSE_C2F; bit-identical results): True / 1 = the

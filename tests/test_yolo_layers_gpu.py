@@ -331,3 +331,44 @@ def test_fused_c2f_is_bit_identical(cuda, H, W, B, variant):
     np.testing.assert_array_equal(r1, r0)
     np.testing.assert_array_equal(s1, s0)
     eng.close()
+
+
+@pytest.mark.parametrize("H,W,B", [(1080, 1920, 3), (640, 640, 2), (360, 640, 1)])
+def test_chained_cv1_is_bit_identical(cuda, H, W, B):
+    """model.3 with model.4.cv1 chained in the same launch (the 1x1 runs on
+    model.3's output tile in LDS; conv_patch_kernel CH form) against the two
+    launches, on the production kernel sequence, default and every autotuned
+    configuration: cv1's output (the y0 | y1 slice of model.4's concat
+    buffer), the raw prediction and the NMS candidates are bit-identical."""
+    from rvs_amd.detect import weights
+    from rvs_amd.detect.yolo_hip import YoloEngine
+    eng = YoloEngine(0, weights.synthetic_weights(0, seed=7), B, (H, W), device=cuda)
+    fr = np.stack([cpu.median(cpu.clahe_ycrcb(road_frame(H, W, seed=40 + b)), 3) for b in range(B)])
+    lb = eng.letterbox(torch.from_numpy(fr).to(cuda))
+    eng.set_raw_fused(True)
+    specs, _ = yolo_ref.conv_specs(0)
+
+    def run(chain, slot):
+        eng.set_fuse_cv1(chain)
+        raw = torch.full((B, 84, eng.A), float("nan"), dtype=torch.float32, device=cuda)
+        eng.forward_raw(lb, raw, slot=slot)
+        torch.cuda.synchronize()
+        ins = Introspect(eng, B)
+        cv1 = None
+        for rec in ins.recs:
+            if specs[rec[0]][0] == "model.4.cv1":
+                cv1 = ins.view(rec[8])[..., rec[10]:rec[10] + specs[rec[0]][2]].copy()
+        assert cv1 is not None
+        return raw.cpu().numpy(), cv1, eng.seg_n[slot].cpu().numpy().copy()
+
+    r0, c0, s0 = run(False, 0)
+    for tuned in (False, True):
+        if tuned:
+            eng.autotune(lb, reps=1)
+        r1, c1, s1 = run(True, 1)
+        np.testing.assert_array_equal(c1, c0)
+        np.testing.assert_array_equal(r1, r0)
+        np.testing.assert_array_equal(s1, s0)
+    # the chained launch is one record of the production launch list
+    assert sum(1 for c in eng.tuned_configs() if c) >= 1
+    eng.close()
