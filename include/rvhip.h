@@ -184,6 +184,14 @@ int rv_yolo_destroy(void* handle);
  * LDS, so that map never reaches HBM; bit-identical to the two launches.
  * Raw parity forwards with RV_YOLO_OPT_RAW_UNFUSED keep them separate. */
 #define RV_YOLO_OPT_FUSE_CV1 5
+/* RV_YOLO_OPT_HEAD_CHAIN (default 0): candidate forwards of the YOLOv8n-
+ * shaped bf16 head run each branch's last 1x1 conv inside its 3x3 conv's
+ * launch (box: + DFL, class: + sigmoid / first maximum) and form the
+ * candidates in one small kernel; the same candidates as the decode
+ * kernel, whose head features and logits then never reach HBM.  Raw
+ * forwards (raw_out) keep the decode kernel.  Off by default: on MI355X the
+ * chained 3x3 launches cost what the decode saves. */
+#define RV_YOLO_OPT_HEAD_CHAIN 6
 int rv_yolo_set_option(void* handle, int opt, int value);
 
 /* fp8 plans (BASELINE configs[4]: "YOLOv8m 1280x1280 fp8 MFMA conv path").

@@ -64,6 +64,11 @@ struct ConvArgs {
   // (out0) is then the 1x1's; the producer's own output stays in LDS.
   const bf16_t* ch_w;
   const float* ch_b;
+  // 1: SiLU, the 1x1's bf16 output stored to out0; 2: a Detect box
+  // branch's last conv, DFL to four f32 distances per pixel (out0: 4 f32
+  // per pixel); 3: a Detect class branch's last conv, sigmoid and first
+  // maximum (out0: {f32 score, i32 class} per pixel)
+  int ch_mode;
 };
 
 // One configuration of the LDS-staged conv kernel: MR x NR 16x16 fragments
@@ -155,6 +160,19 @@ struct HeadLevel {
   float* logits_out;
 };
 
+// The chained Detect head's outputs per level (conv_patch_kernel ch_mode 2 /
+// 3): bx = 4 f32 DFL distances per pixel, sc = {f32 score, i32 class} per
+// pixel, B x H x W each; start / blk: first anchor / first 64-anchor
+// segment of each level (+ totals at [nlv]).
+struct HeadCombine {
+  const float* bx[4];
+  const float* sc[4];
+  int H[4], W[4];
+  float stride[4];
+  int start[5], blk[5];
+  int nlv;
+};
+
 struct Cand {  // one detection candidate (Ultralytics NMS row before NMS)
   float x1, y1, x2, y2, score;
   int cls, anchor, pad;
@@ -168,5 +186,10 @@ struct Cand {  // one detection candidate (Ultralytics NMS row before NMS)
 int decode_segments(const HeadLevel* lv, int nlv);
 int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_max, float conf,
                          float* raw, Cand* cand, int cand_cap, int* seg_n, hipStream_t s);
+
+// Candidates of the chained head (HeadCombine): the fixed decode's output
+// for the same logits, in the segmented layout of rv_yolo_forward.
+int launch_head_combine(const HeadCombine& h, int B, float conf, Cand* cand, int cand_cap,
+                        int* cand_n, hipStream_t s);
 
 }  // namespace rv

@@ -335,6 +335,13 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint3
                                            (int)voff, soff, 0, AUX);
 }
 
+// Detect-head class score: exp + one v_rcp_f32 (no IEEE division
+// sequence); the decode, its raw output and the chained head epilogue
+// (conv_patch_kernel CHM = 3) all use this one function.
+__device__ __forceinline__ float head_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+
 struct PatchGeo {
   int C, R;        // output tile cols / rows (R*C <= 64*NR)
   int G;           // input-channel chunks per pipeline stage
@@ -718,11 +725,14 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& a, f32x4 (&acc)[MR][NR
 // so a resident weight slab (or a staged chunk of weights) is shared by 8
 // waves and the pixel tile is twice as large -- half the LDS-DMA bytes per
 // MFMA of the 4-wave form at the same occupancy (2 waves per SIMD).
-// CH = true (ConvArgs::ch_w): a chained 1x1 conv Cout -> Cout (a C2f cv1
-// fused into the conv producing its input; bf16, one cout tile covering
-// Cout, MR even): see chain_tile below.
-template <int MR, int NR, int K, int S, bool RESW, bool F8, int NW = 4, bool CH = false>
+// CHM > 0 (ConvArgs::ch_w / ch_mode): a chained 1x1 conv Cout -> Cout on
+// the tile's output in LDS (bf16, one cout tile covering Cout): CHM 1 = a
+// C2f cv1 (SiLU, stored), 2 = a Detect box branch's last conv + DFL (four
+// distances per pixel stored), 3 = a Detect class branch's last conv +
+// sigmoid + first maximum (score, class per pixel stored): see chain_tile.
+template <int MR, int NR, int K, int S, bool RESW, bool F8, int NW = 4, int CHM = 0>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(ConvArgs a, PatchGeo g) {
+  constexpr bool CH = CHM != 0;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int T2 = K * K;
   constexpr int BC = 16 * MR;
@@ -835,21 +845,32 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
   // swizzle of conv1x1_direct_kernel), its bias, and one x tile per wave
   // (the wave's 16 NR pixels x Cout channels of the producer's bf16 output,
   // chunk-major [c][pixel][64 B], quarter swizzle by pixel)
-  constexpr int CHN = MR / 2;                       // 32-channel chunks of the chained input
+  constexpr int CHN = (MR + 1) / 2;                 // 32-channel chunks of the chained input
+  constexpr int CHF = BC + 4;                       // CHM 2: floats per pixel row of the logit tile
   uint8_t* const ch_w_lds = (uint8_t*)(bias_lds + BC);
   float* const ch_b_lds = (float*)(ch_w_lds + (CH ? CHN * BC * 64 : 0));
   uint8_t* const ch_x_lds = (uint8_t*)(ch_b_lds + (CH ? BC : 0)) + wave * (CH ? CHN * NR * 16 * 64 : 0);
+  float* const ch_f_lds = (float*)((uint8_t*)(ch_b_lds + (CH ? BC : 0)) + NW * (CH ? CHN * NR * 16 * 64 : 0)) +
+                          wave * (CHM == 2 ? NR * 16 * CHF : 0);
   if constexpr (CH) {
-    static_assert(!F8 && MR % 2 == 0, "chained 1x1: bf16, whole 32-channel chunks");
-    // BC / 16 DMA instructions per chunk (16 rows x 64 B each)
+    static_assert(!F8 && K == 3, "chained 1x1: bf16 behind a 3x3 conv");
+    // BC / 16 DMA instructions per chunk (16 rows x 64 B each); the packed
+    // 1x1 rows are CHN * 32 channels long (zero beyond Cout)
     for (int j = wave; j < CHN * (BC / 16); j += NW) {
       const int c = j / (BC / 16), jr = j - c * (BC / 16);
       const int row = jr * 16 + (lane >> 2);
       const int q = (lane & 3) ^ swzq<false>(row);
-      __builtin_amdgcn_global_load_lds((const void*)(a.ch_w + (size_t)row * BC + c * 32 + q * 8),
+      __builtin_amdgcn_global_load_lds((const void*)(a.ch_w + (size_t)row * (CHN * 32) + c * 32 + q * 8),
                                        (void*)(ch_w_lds + c * BC * 64 + jr * 1024), 16, 0, 0);
     }
     for (int i = tid; i < BC; i += 64 * NW) ch_b_lds[i] = a.ch_b[i];
+    if constexpr (MR % 2) {  // odd MR: the last chunk's upper half is k-padding, zero for good
+      for (int px = lane; px < NR * 16; px += 64) {
+        uint8_t* sl = ch_x_lds + ((CHN - 1) * NR * 16 + px) * 64;
+        *(uint4*)(sl + ((2 ^ swzq<false>(px)) << 4)) = make_uint4(0, 0, 0, 0);
+        *(uint4*)(sl + ((3 ^ swzq<false>(px)) << 4)) = make_uint4(0, 0, 0, 0);
+      }
+    }
   }
   // Patch and weight DMA through buffer resources (buffer_load ... lds):
   // every DMA instruction's per-lane byte offset is computed once -- per
@@ -1126,6 +1147,22 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
     if constexpr (CH) {
       f32x4 bl[MR];
       bias_tile(bl);
+      if constexpr (MR % 2) {  // odd MR: each lane stores its 4 channels (8 B) of every fragment
+#pragma unroll
+        for (int n = 0; n < NR; ++n) {
+          const int px = n * 16 + col;
+#pragma unroll
+          for (int m = 0; m < MR; ++m) {
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = acc[m][n][i] + bl[m][i];
+            if (a.act) silu4(v);
+            const int qq = 2 * (m & 1) + (quad >> 1);  // channels 16 (m & 1) + 4 quad of chunk m / 2
+            *(v2u32*)(ch_x_lds + ((m / 2) * NR * 16 + px) * 64 + ((qq ^ swzq<false>(px)) << 4) +
+                      (quad & 1) * 8) = v2u32{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+          }
+        }
+      } else {
 #pragma unroll
       for (int n = 0; n < NR; ++n) {
         const int px = n * 16 + col;
@@ -1148,6 +1185,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
           *(v4u32*)(ch_x_lds + ((m / 2) * NR * 16 + px) * 64 + ((qq ^ swzq<false>(px)) << 4)) =
               v4u32{x0[0], x1[0], x0[1], x1[1]};
         }
+      }
       }
       f32x4 acc2[MR][NR];
 #pragma unroll
@@ -1178,10 +1216,93 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
       f32x4 bl2[MR];
 #pragma unroll
       for (int m = 0; m < MR; ++m) bl2[m] = *(const f32x4*)(ch_b_lds + m * 16 + quad * 4);
-      ConvArgs a2 = a;
-      a2.act = 1;
-      a2.res = nullptr;
-      epilogue_fast<MR, NR>(a2, acc2, 0, pv, opx, quad, bl2);
+      if constexpr (CHM == 1) {
+        ConvArgs a2 = a;
+        a2.act = 1;
+        a2.res = nullptr;
+        epilogue_fast<MR, NR>(a2, acc2, 0, pv, opx, quad, bl2);
+      } else if constexpr (CHM == 2) {
+        // box branch: 4 sides x 16 DFL bins (fragment m = side m).  The f32
+        // logits go to this wave's LDS rows, then 4 lanes per pixel take a
+        // side each: softmax expectation over its bins exactly as
+        // detect_decode_kernel computes it (same op order), and the pixel's
+        // four distances are stored as one f32x4
+        static_assert(MR == 4, "box branch: 4 sides of 16 bins");
+#pragma unroll
+        for (int n = 0; n < NR; ++n)
+#pragma unroll
+          for (int m = 0; m < MR; ++m)
+            *(f32x4*)(ch_f_lds + (n * 16 + col) * CHF + m * 16 + quad * 4) = acc2[m][n] + bl2[m];
+        const int pxl = lane >> 2, part = lane & 3;
+#pragma unroll
+        for (int n = 0; n < NR; ++n) {
+          const float* row = ch_f_lds + (n * 16 + pxl) * CHF + part * 16;
+          float v[16];
+#pragma unroll
+          for (int i = 0; i < 16; i += 4) {
+            const f32x4 q4 = *(const f32x4*)(row + i);
+            v[i] = q4[0];
+            v[i + 1] = q4[1];
+            v[i + 2] = q4[2];
+            v[i + 3] = q4[3];
+          }
+          float mx = -INFINITY;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) mx = fmaxf(mx, v[i]);
+          float sum = 0.f;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            v[i] = __expf(v[i] - mx);
+            sum += v[i];
+          }
+          const float rs = __builtin_amdgcn_rcpf(sum);
+          float e = 0.f;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) e += (float)i * (v[i] * rs);
+          const int base = lane & ~3;
+          const float d0 = __shfl(e, base), d1 = __shfl(e, base + 1), d2 = __shfl(e, base + 2),
+                      d3 = __shfl(e, base + 3);
+          // pixel pxl of fragment n: lane pxl holds its validity and index
+          const uint32_t o = (uint32_t)__shfl((int)opx[n], pxl);
+          const bool ok = __shfl((int)pv[n], pxl) != 0;
+          if (part == 0 && ok) *(f32x4*)((float*)a.out0 + (size_t)o * 4) = f32x4{d0, d1, d2, d3};
+        }
+      } else {
+        // class branch: sigmoid of every class, the first maximum in class
+        // order (lane scan over its classes m * 16 + 4 quad + i ascending,
+        // then the larger score / smaller class across the quads) -- the
+        // fixed decode's head_mfma_fixed selection; (score, class) stored
+#pragma unroll
+        for (int n = 0; n < NR; ++n) {
+          float best = -1.f;
+          int bc = 0;
+#pragma unroll
+          for (int m = 0; m < MR; ++m) {
+            const int co = m * 16 + quad * 4;
+            const f32x4 v = acc2[m][n] + bl2[m];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float sg = head_sigmoid(v[i]);
+              if (co + i < a.Cout && sg > best) {
+                best = sg;
+                bc = co + i;
+              }
+            }
+          }
+#pragma unroll
+          for (int off = 16; off < 64; off <<= 1) {
+            const float ob = __shfl_xor(best, off);
+            const int oc = __shfl_xor(bc, off);
+            if (ob > best || (ob == best && oc < bc)) {
+              best = ob;
+              bc = oc;
+            }
+          }
+          if (quad == 0 && pv[n])
+            *(v2u32*)((float*)a.out0 + (size_t)opx[n] * 2) =
+                v2u32{__float_as_uint(best), (uint32_t)bc};
+        }
+      }
     }
   };
   auto finish = [&](int tile, EpiPend<MR, NR>& ep, bool pk) {
@@ -1506,8 +1627,11 @@ static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& 
   // two stages: the next (tile, chunk group) streams in during the current one
   smem = (c.resw ? nch * wb : 0) + 2 * (size_t)g.G * (g.p_bytes + (c.resw ? 0 : wb)) +
          (a.in8 ? 0 : (size_t)16 * MR * 4);  // bf16: the block's bias
-  if (a.ch_w)  // chained 1x1: its weights and bias, one x tile per wave
-    smem += (size_t)(MR / 2) * 16 * MR * 64 + (size_t)16 * MR * 4 + (size_t)NW * (MR / 2) * NR * 16 * 64;
+  if (a.ch_w) {  // chained 1x1: its weights and bias, one x tile per wave (+ logit rows)
+    const size_t chn = (MR + 1) / 2;
+    smem += chn * 16 * MR * 64 + (size_t)16 * MR * 4 + (size_t)NW * chn * NR * 16 * 64 +
+            (a.ch_mode == 2 ? (size_t)NW * NR * 16 * (16 * MR + 4) * 4 : 0);
+  }
   return smem <= 160 * 1024;
 }
 
@@ -1527,11 +1651,11 @@ static int num_cus() {
 
 // Every instantiation gets the full 160 KB dynamic-LDS cap once; resident
 // blocks per CU are cached per LDS size (per instantiation).
-template <int MR, int NR, int K, int S, bool RESW, bool F8 = false, int NW = 4, bool CH = false>
+template <int MR, int NR, int K, int S, bool RESW, bool F8 = false, int NW = 4, int CHM = 0>
 static int launch_patch_t(const ConvArgs& a, const PatchGeo& g, size_t smem, int persist,
                           hipStream_t s) {
   static bool attr = false;
-  auto fn = conv_patch_kernel<MR, NR, K, S, RESW, F8, NW, CH>;
+  auto fn = conv_patch_kernel<MR, NR, K, S, RESW, F8, NW, CHM>;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        160 * 1024);
@@ -1646,21 +1770,34 @@ constexpr bool patch_spills8(int MR, int NR, int K, int S, bool RESW) {
                     (S == 2 && !RESW && MR == 1 && NR == 2));
 }
 
-// chained-1x1 (CH) instantiations: C2f cv1 behind a 64-channel 3x3 conv
-// (YOLOv8n model.3 -> model.4.cv1); ch_tile_ok is the host-side check
-template <int MR, int NR>
+// chained-1x1 (CHM) instantiations: C2f cv1 behind a 64-channel 3x3 conv
+// (YOLOv8n model.3 -> model.4.cv1, mode 1, stride 2), the Detect box /
+// class branches' last convs behind their 3x3 (.1 -> .2: mode 2 with 64
+// channels, mode 3 with 80, stride 1); ch_tile_ok is the host-side check
+template <int MR, int NR, int CHM>
 constexpr bool ch_built() {
-  return MR == 4 && NR <= 2;
+  return NR <= 2 && ((CHM <= 2 && MR == 4) || (CHM == 3 && MR == 5));
 }
-static bool ch_tile_ok(int mr, int nr) { return mr == 4 && nr <= 2; }
+static bool ch_tile_ok(int mr, int nr, int mode) {
+  return nr <= 2 && ((mode <= 2 && mr == 4) || (mode == 3 && mr == 5));
+}
 template <int MR, int NR, bool RESW, int NW>
 static int launch_patch_ch(const ConvArgs& a, const PatchGeo& g, size_t smem, int persist,
                            hipStream_t s) {
-  if constexpr (ch_built<MR, NR>()) {
-    if (a.k == 3 && a.stride == 2) return launch_patch_t<MR, NR, 3, 2, RESW, false, NW, true>(a, g, smem, persist, s);
-    if (a.k == 3 && a.stride == 1) return launch_patch_t<MR, NR, 3, 1, RESW, false, NW, true>(a, g, smem, persist, s);
+  if constexpr (ch_built<MR, NR, 1>()) {
+    if (a.ch_mode == 1 && a.k == 3 && a.stride == 2)
+      return launch_patch_t<MR, NR, 3, 2, RESW, false, NW, 1>(a, g, smem, persist, s);
+    if (a.ch_mode == 1 && a.k == 3 && a.stride == 1)
+      return launch_patch_t<MR, NR, 3, 1, RESW, false, NW, 1>(a, g, smem, persist, s);
   }
-  set_error("conv_patch (chained 1x1): no variant MR=%d NR=%d k=%d s=%d", MR, NR, a.k, a.stride);
+  if constexpr (ch_built<MR, NR, 2>())
+    if (a.ch_mode == 2 && a.k == 3 && a.stride == 1)
+      return launch_patch_t<MR, NR, 3, 1, RESW, false, NW, 2>(a, g, smem, persist, s);
+  if constexpr (ch_built<MR, NR, 3>())
+    if (a.ch_mode == 3 && a.k == 3 && a.stride == 1)
+      return launch_patch_t<MR, NR, 3, 1, RESW, false, NW, 3>(a, g, smem, persist, s);
+  set_error("conv_patch (chained 1x1 mode %d): no variant MR=%d NR=%d k=%d s=%d", a.ch_mode, MR, NR,
+            a.k, a.stride);
   return RV_EINVAL;
 }
 
@@ -1725,9 +1862,9 @@ static const int kTiles[][2] = {{8, 2}, {8, 1}, {5, 2}, {5, 1}, {4, 4}, {4, 2}, 
                                 {2, 4}, {2, 2}, {2, 1}, {1, 4}, {1, 2}, {1, 1}};
 
 bool conv_cfg_ok(const ConvArgs& a, const ConvCfg& c) {
-  if (a.ch_w &&  // chained 1x1: the patch kernel's CH form, one cout tile, fast epilogue
-      (c.kind == 1 || a.in8 || !ch_tile_ok(c.mr, c.nr) || 16 * c.mr != a.Cout || a.k != 3 ||
-       a.res || a.out1 || a.out0_up || !epi_fast(a) || a.g2_cout0 > 0 || vcat(a)))
+  if (a.ch_w &&  // chained 1x1: the patch kernel's CHM form, one cout tile covering Cout
+      (c.kind == 1 || a.in8 || !ch_tile_ok(c.mr, c.nr, a.ch_mode) || 16 * c.mr < a.Cout || 16 * c.mr - a.Cout >= 16 || a.k != 3 || a.res || a.out1 || a.out0_up || a.g2_cout0 > 0 ||
+       vcat(a) || (a.ch_mode == 1 ? !epi_fast(a) : (!a.out_f32 || a.stride != 1))))
     return false;
   if (c.kind == 1) return !a.in8 && direct_ok(a, c);
   if ((c.kind != 0 && c.kind != 2) || vcat(a)) return false;
@@ -2087,9 +2224,7 @@ struct HeadLevels {
 // Class score: exp + one v_rcp_f32 (no IEEE division sequence).  The raw
 // output and the candidate filter use this same function, so the scores NMS
 // sees are the scores in `raw`.
-__device__ __forceinline__ float head_sigmoid(float x) {
-  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
-}
+// (head_sigmoid: defined with the patch kernel's chained head epilogue)
 
 // The fused head's MFMA section with compile-time trip counts (KB box /
 // KC class 32-channel k-steps, NCF class fragments: YOLOv8n's head is
@@ -2474,6 +2609,86 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(HeadLevels h, int B,
       }
     }
   }
+}
+
+// The chained head's last step (ConvArgs::ch_mode 2 / 3 wrote, per level
+// pixel, the four DFL distances and the best class (score, class)): one
+// wave per 64-anchor segment of one image -- dist2bbox * stride,
+// xywh2xyxy and the conf filter with the expressions of
+// detect_decode_kernel, candidates in the same segmented layout and anchor
+// order (ballot ranks), so its output equals the fixed decode's.
+__global__ __launch_bounds__(256) void head_combine_kernel(HeadCombine h, int B, float conf,
+                                                           Cand* __restrict__ cand, int cap,
+                                                           int* __restrict__ seg_n, int nblk) {
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);  // wave-uniform
+  if (blk >= nblk) return;
+  int l = 0;
+#pragma unroll
+  for (int i = 1; i < 4; ++i)
+    if (i < h.nlv && blk >= h.blk[i]) l = i;
+  // compile-time selection of the level's fields (no dynamic index into
+  // the by-value argument)
+  const float* bx = h.bx[0];
+  const float* sc = h.sc[0];
+  int W = h.W[0], HW = h.H[0] * h.W[0], lstart = h.start[0], lblk = h.blk[0];
+  float stride = h.stride[0];
+#pragma unroll
+  for (int i = 1; i < 4; ++i)
+    if (i == l) {
+      bx = h.bx[i];
+      sc = h.sc[i];
+      W = h.W[i];
+      HW = h.H[i] * h.W[i];
+      lstart = h.start[i];
+      lblk = h.blk[i];
+      stride = h.stride[i];
+    }
+  const int r0 = (blk - lblk) * 64;
+  const bool live = r0 + lane < HW;
+  const int r = r0 + (live ? lane : 0);
+  const f32x4 d = *(const f32x4*)(bx + ((size_t)b * HW + r) * 4);
+  const v2u32 q = *(const v2u32*)(sc + ((size_t)b * HW + r) * 2);
+  const float best = __uint_as_float(q[0]);
+  const int bc = (int)q[1];
+  const int a = lstart + r;
+  const int y = r / W, x = r - (r / W) * W;
+  const float ax = (float)x + 0.5f, ay = (float)y + 0.5f;
+  const float x1 = ax - d[0], y1 = ay - d[1], x2 = ax + d[2], y2 = ay + d[3];
+  const float cx = (x1 + x2) / 2.0f * stride, cy = (y1 + y2) / 2.0f * stride;
+  const float w = (x2 - x1) * stride, hh = (y2 - y1) * stride;
+  const bool pass = live && best > conf;
+  const unsigned long long m = __ballot(pass);
+  if (lane == 0) seg_n[(size_t)b * nblk + blk] = __popcll(m);
+  if (pass) {
+    const int i = blk * 64 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (i < cap) {
+      const float hw = w / 2.0f, hh2 = hh / 2.0f;  // xywh2xyxy
+      Cand c;
+      c.x1 = cx - hw;
+      c.y1 = cy - hh2;
+      c.x2 = cx + hw;
+      c.y2 = cy + hh2;
+      c.score = best;
+      c.cls = bc;
+      c.anchor = a;
+      c.pad = 0;
+      cand[(size_t)b * cap + i] = c;
+    }
+  }
+}
+
+int launch_head_combine(const HeadCombine& h, int B, float conf, Cand* cand, int cand_cap,
+                        int* cand_n, hipStream_t s) {
+  const int nblk = h.blk[h.nlv];
+  if (!cand || !cand_n || cand_cap < nblk * 64) {
+    set_error("head combine: candidate buffers (cap %d < %d segments x 64)", cand_cap, nblk);
+    return RV_EINVAL;
+  }
+  head_combine_kernel<<<dim3(ceil_div(nblk, 4), B), 256, 0, s>>>(h, B, conf, cand, cand_cap, cand_n, nblk);
+  return launch_status("head_combine");
 }
 
 int decode_segments(const HeadLevel* lv, int nlv) {

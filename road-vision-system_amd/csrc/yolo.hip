@@ -345,6 +345,7 @@ struct Model {
   int stem_x1 = 0;
   int head_streams = 1;            // RV_YOLO_OPT_HEAD_STREAMS
   int fuse_cv1 = 1;                // RV_YOLO_OPT_FUSE_CV1
+  int head_chain = 0;              // RV_YOLO_OPT_HEAD_CHAIN (measured neutral: DESIGN.md)
   std::vector<Buf> bufs;
   int nA = 0;
   int map_h[6], map_w[6];  // stride 2^i maps
@@ -368,6 +369,7 @@ struct Model {
   int X0, X1, C2, X2, X3, C4, CAT14, X5, C6, CAT11, X7, C8, X8, SP, CAT20, C12, CAT17, C15,
       X15, C18, X18, C21, X21;
   int DA[3], DB[3], HD[3];
+  int BX[3], SC[3];  // chained head: DFL distances / (score, class) per pixel
 
   size_t ws_bytes(int B) const {
     size_t off = 0;
@@ -411,6 +413,8 @@ static void plan(Model& M) {
     M.DA[i] = M.newbuf("DA" + l, 3 + i, v.c2d + v.c3d);
     M.DB[i] = M.newbuf("DB" + l, 3 + i, v.c2d + v.c3d, false, true);  // bf16: the decode's features
     M.HD[i] = M.newbuf("HD" + l, 3 + i, 4 * v.reg + v.nc, true);
+    M.BX[i] = M.newbuf("BX" + l, 3 + i, 4, true);
+    M.SC[i] = M.newbuf("SC" + l, 3 + i, 2, true);
   }
   // one temp per bottleneck (its first conv's output): no buffer is ever
   // overwritten inside a forward, so every layer stays inspectable
@@ -690,10 +694,42 @@ struct Exec {
     ConvCfg probe{4, 1, 1, 1, 1, 0};
     a.ch_w = wptr(c2);
     a.ch_b = bptr(c2);
+    a.ch_mode = 1;
     if (!conv_cfg_ok(a, probe)) return false;
     // trace records: the two convs as the unfused plan runs them
     trace(i1, args(c1, in, li, mid, 0, none, 0, none), in, mid, 0, none, 0, none);
     const ConvArgs a2 = args(c2, mid, li + 1, o0, 0, none, 0, none);
+    trace(i2, a2, mid, o0, 0, none, 0, none);
+    launch(a, i1, flops_of(c1, a) + flops_of(c2, a2));
+    return true;
+  }
+
+  // The Detect head's branch of level li: its 3x3 conv n1 (input view in,
+  // nominal output `mid` -- never written) with its last 1x1 conv n2
+  // chained in the same launch (ch_mode 2: box, DFL distances to o0; 3:
+  // class, best (score, class) to o0).  probe_only: just report whether the
+  // shapes have a chained configuration.
+  bool head_chain(const std::string& n1, View in, int li, View mid, const std::string& n2,
+                  View o0, int mode, bool probe_only) {
+    if (status) return false;
+    const int i1 = M->def.find(n1), i2 = M->def.find(n2);
+    if (i1 < 0 || i2 < 0) return false;
+    const ConvSpec& c1 = M->def.convs[i1];
+    const ConvSpec& c2 = M->def.convs[i2];
+    if (c1.f8 || c2.f8 || c1.k != 3 || c1.s != 1 || c2.k != 1 || c2.cin != c1.cout ||
+        c2.cout != c1.cout || !c1.act || c2.act || c1.cout != (mode == 2 ? 64 : 80))
+      return false;
+    const View none{-1, 0, 0};
+    ConvArgs a = args(c1, in, li, o0, 0, none, 0, none);
+    a.ch_w = wptr(c2);
+    a.ch_b = bptr(c2);
+    a.ch_mode = mode;
+    if (!conv_cfg_ok(a, ConvCfg{mode == 2 ? 4 : 5, 1, 1, 1, 1, 0}) &&
+        !conv_cfg_ok(a, ConvCfg{mode == 2 ? 4 : 5, 1, 1, 0, 1, 0}))
+      return false;
+    if (probe_only) return true;
+    trace(i1, args(c1, in, li, mid, 0, none, 0, none), in, mid, 0, none, 0, none);
+    const ConvArgs a2 = args(c2, mid, li, o0, 0, none, 0, none);
     trace(i2, a2, mid, o0, 0, none, 0, none);
     launch(a, i1, flops_of(c1, a) + flops_of(c2, a2));
     return true;
@@ -983,6 +1019,9 @@ extern "C" int rv_yolo_set_option(void* h, int opt, int value) {
     case RV_YOLO_OPT_FUSE_CV1:
       M->fuse_cv1 = value != 0;
       return RV_OK;
+    case RV_YOLO_OPT_HEAD_CHAIN:
+      M->head_chain = value != 0;
+      return RV_OK;
     default:
       set_error("unknown yolo option %d", opt);
       return RV_EINVAL;
@@ -1257,9 +1296,33 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
   const bool fork = streams_on && B >= 8 && M->side[0] && M->side[1] &&
                     !(M->prof.on && M->prof.n_fwd < M->prof.cap_fwd);
   const hipStream_t main_s = E.s;
+  // The chained head (RV_YOLO_OPT_HEAD_CHAIN; RV_HEAD_CHAIN=0/1 overrides):
+  // each branch's .1 conv runs its .2 1x1 on the tile in LDS and keeps only
+  // the DFL distances (box) / the best (score, class) (class), and one small
+  // kernel (head_combine_kernel) forms the candidates -- the DB features and
+  // the f32 logits never reach HBM.  Candidate forwards of the bf16
+  // YOLOv8n-shaped head only (raw forwards keep the decode kernel); the same
+  // candidates as the fixed decode.
+  static const int chain_env = getenv("RV_HEAD_CHAIN") ? atoi(getenv("RV_HEAD_CHAIN")) : -1;
+  bool hchain = (chain_env < 0 ? M->head_chain != 0 : chain_env != 0) && !f8 && fuse_head && !raw_out && cand && v.nc == 80 &&
+                v.reg == 16 && v.c2d == 64 && v.c3d == 80;
+  for (int i = 0; i < 3 && hchain; ++i) {
+    const std::string a = "model.22.cv2." + std::to_string(i), c = "model.22.cv3." + std::to_string(i);
+    hchain = E.head_chain(a + ".1", View{M->DA[i], dcs, 0}, 3 + i, View{M->DB[i], dcs, 0}, a + ".2",
+                          View{M->BX[i], 4, 0}, 2, true) &&
+             E.head_chain(c + ".1", View{M->DA[i], dcs, v.c2d}, 3 + i, View{M->DB[i], dcs, v.c2d},
+                          c + ".2", View{M->SC[i], 2, 0}, 3, true);
+  }
   auto head_level = [&](int i) {
     const std::string a = "model.22.cv2." + std::to_string(i), c = "model.22.cv3." + std::to_string(i);
     E.conv_pair(a + ".0", P[i], c + ".0", P[i], 3 + i, View{M->DA[i], dcs, 0});
+    if (hchain) {
+      E.head_chain(a + ".1", View{M->DA[i], dcs, 0}, 3 + i, View{M->DB[i], dcs, 0}, a + ".2",
+                   View{M->BX[i], 4, 0}, 2, false);
+      E.head_chain(c + ".1", View{M->DA[i], dcs, v.c2d}, 3 + i, View{M->DB[i], dcs, v.c2d}, c + ".2",
+                   View{M->SC[i], 2, 0}, 3, false);
+      return E.status;
+    }
     E.conv_pair(a + ".1", View{M->DA[i], dcs, 0}, c + ".1", View{M->DA[i], dcs, v.c2d}, 3 + i,
                 View{M->DB[i], dcs, 0});
     if (!fuse_head) {
@@ -1305,6 +1368,21 @@ extern "C" int rv_yolo_forward_part(void* h, const uint8_t* lb, int B, void* ws,
       E.status = hip_check(hipStreamWaitEvent(main_s, M->ev_join[i], 0), "head join wait");
   if (E.status) return E.status;
   if (M->prof.on && M->prof.n_fwd < M->prof.cap_fwd) M->prof.n_fwd++;
+  if (hchain) {
+    HeadCombine hc;
+    memset(&hc, 0, sizeof(hc));
+    hc.nlv = 3;
+    for (int i = 0; i < 3; ++i) {
+      hc.bx[i] = (const float*)E.ptr(M->BX[i]);
+      hc.sc[i] = (const float*)E.ptr(M->SC[i]);
+      hc.H[i] = M->map_h[3 + i];
+      hc.W[i] = M->map_w[3 + i];
+      hc.stride[i] = (float)(8 << i);
+      hc.start[i + 1] = hc.start[i] + hc.H[i] * hc.W[i];
+      hc.blk[i + 1] = hc.blk[i] + ceil_div(hc.H[i] * hc.W[i], 64);
+    }
+    return launch_head_combine(hc, B, conf, (Cand*)cand, cand_cap, cand_n, E.s);
+  }
   HeadLevel hl[3];
   memset(hl, 0, sizeof(hl));
   for (int i = 0; i < 3; ++i) {

@@ -219,6 +219,14 @@ class YoloEngine:
         for h in self._hs:
             call("rv_yolo_set_option", h, 5, 1 if on else 0)
 
+    def set_head_chain(self, on: bool) -> None:
+        """Candidate forwards run each Detect branch's last 1x1 conv inside
+        its 3x3 conv's launch plus one small combine kernel (True, default)
+        or through the decode kernel (RV_YOLO_OPT_HEAD_CHAIN; the same
+        candidates)."""
+        for h in self._hs:
+            call("rv_yolo_set_option", h, 6, 1 if on else 0)
+
     def set_fuse_c2f(self, on) -> None:
         """Narrow C2f blocks as one fused launch or one launch per conv
         (RV_YOLO_OPT_FUSE_C2F; bit-identical results): True / 1 = the

@@ -167,7 +167,9 @@ def test_first_conv_sppf_and_decode(cuda):
     for j, p in enumerate((p1, p2, p3)):
         np.testing.assert_array_equal(s[..., (j + 1) * c:(j + 2) * c], p.numpy().transpose(0, 2, 3, 1))
     # decode from the GPU's own head logits
-    heads = [i for i, bb in enumerate(ins.bufs) if bb[3] == 1]
+    # (the f32 logit maps: 4 * reg_max + nc channels; the chained head's
+    # small f32 maps -- DFL distances, (score, class) -- are not logits)
+    heads = [i for i, bb in enumerate(ins.bufs) if bb[3] == 1 and bb[2] == 4 * 16 + 80]
     assert len(heads) == 3
     outs, anc, st = [], [], []
     for lvl, hb in enumerate(heads):
@@ -371,4 +373,43 @@ def test_chained_cv1_is_bit_identical(cuda, H, W, B):
         np.testing.assert_array_equal(s1, s0)
     # the chained launch is one record of the production launch list
     assert sum(1 for c in eng.tuned_configs() if c) >= 1
+    eng.close()
+
+
+@pytest.mark.parametrize("H,W,B", [(1080, 1920, 4), (640, 640, 2), (360, 640, 3)])
+def test_chained_head_matches_decode(cuda, H, W, B):
+    """The chained Detect head (each branch's last 1x1 conv in its 3x3
+    conv's launch: box + DFL, class + sigmoid / first maximum; then the
+    combine kernel) against the decode kernel on the same forward: every
+    segment's candidate count and rows, and the NMS output, bit-identical
+    -- default and autotuned conv configurations."""
+    from rvs_amd.detect import weights
+    from rvs_amd.detect.yolo_hip import YoloEngine
+    eng = YoloEngine(0, weights.synthetic_weights(0, seed=11), B, (H, W), device=cuda)
+    fr = np.stack([cpu.median(cpu.clahe_ycrcb(road_frame(H, W, seed=60 + b)), 3) for b in range(B)])
+    lb = eng.letterbox(torch.from_numpy(fr).to(cuda))
+
+    def run(chain, slot):
+        eng.set_head_chain(chain)
+        eng.seg_n[slot].fill_(-7)
+        eng.forward_raw(lb, slot=slot)
+        dets, n = eng.nms(B, slot)
+        torch.cuda.synchronize()
+        nseg = eng.nseg
+        seg = eng.seg_n[slot].view(-1)[:B * nseg].view(B, nseg).cpu().numpy().copy()
+        cand = eng.cand[slot][:B].cpu().numpy().view(np.uint32).reshape(B, eng.cap, -1)
+        rows = [cand[b, 64 * j:64 * j + seg[b, j]].copy() for b in range(B) for j in range(nseg)]
+        return seg, rows, dets.cpu().numpy().copy(), n.cpu().numpy().copy()
+
+    s0, r0, d0, n0 = run(False, 0)
+    assert s0.min() >= 0 and s0.sum() > 0
+    for tuned in (False, True):
+        if tuned:
+            eng.autotune(lb, reps=1)
+        s1, r1, d1, n1 = run(True, 1)
+        np.testing.assert_array_equal(s1, s0)
+        for a, b in zip(r1, r0):
+            np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(n1, n0)
+        np.testing.assert_array_equal(d1.view(np.uint32), d0.view(np.uint32))
     eng.close()
