@@ -199,8 +199,8 @@ int launch_conv0_fp8(const uint8_t* img, int B, int H, int W, const Conv0Q& q, i
 // even c + 1 with zero weights for the phantom -- so 16 consecutive X1
 // pixels read 16 consecutive 32-B stored pixels of one region.
 // Swizzle: 16-B half h of stored pixel s sits at s * 32 + 16 (h ^ bit 2 of
-// s).  conv0 writes a pixel's half as one 16-B store (fragments f and f + 4
-// of a wave exchange their quad 0/1 and 2/3 channel quarters with
+// s).  conv0 writes a pixel's half as one 16-B store (the two fragments
+// of a pair exchange their quad 0/1 and 2/3 channel quarters with
 // v_permlane16_swap first), and 8 consecutive pixels of a ds_write_b128 lane
 // group then cover all 32 banks; in model.1's ds_read_b128 lane groups the
 // 16 lanes hit 16 distinct 16-B bank slots for any row (72 = 0 mod 8 keeps
@@ -223,8 +223,9 @@ constexpr int kStXW = 2 * kStC + 1;          // X0 pixels per tile row (33 even 
 constexpr int kStXS = 72;                    // stored pixel slots per row (a multiple of 8)
 constexpr int kStRowB = kStXS * 32;          // 2304 B per X0 tile row
 constexpr int kStXB = kStXR * kStRowB;       // 39,168 B (4 blocks / CU)
-constexpr int kStNpx = kStXR * kStXW;        // 1105 X0 pixels per tile
-constexpr int kStNfr = (kStNpx + 15) / 16;   // 70 conv0 fragments
+constexpr int kStNpx = kStXR * kStXW;        // 1105 X0 pixels per tile: 70 conv0 fragments
+static_assert(kStXE == 33 && kStXW - kStXE == 32 && kStXR % 2 == 1,
+              "conv0 strips: 2 x 16 even + 2 x 16 odd columns, 9 row pairs");
 
 __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ img, int B, int H,
                                                    int W, Conv0Q q0,
@@ -250,46 +251,63 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(img + (size_t)b * H * W * 3), 0, H * W * 3, kRsrcFlags);
 
-  // ---- 1. conv0 over the X0 tile: fragment f = tile pixels t = 16 f .. +15
-  //      (row t / 65, stored column t % 65); wave w runs the pairs (f, f + 4),
-  //      f = w + 8 i, and stores each pixel's 16-B halves (see the swizzle)
+  // ---- 1. conv0 over the X0 tile.  Wave w owns one 16-column strip of
+  //      the tile for all 17 rows: stored columns 16 w + col (w = 0, 1: even
+  //      X0 columns, xr = 2 j) or 33 + 16 (w - 2) + col (w = 2, 3: odd, xr =
+  //      2 (j - 33) + 1).  Pair i = tile rows 2 i (fragment a) and 2 i + 1
+  //      (b).  The strip's column, window alignment and column checks are lane
+  //      constants and a pair's rows are wave-uniform, so a window costs a
+  //      compare, an add and two selects, and the unrolled pairs store at
+  //      immediate offsets.  Pair 8 holds row 16 only; its b fragment is the
+  //      17 pixels of even stored column 32 (xr = 64): rows 0-15 on wave 0,
+  //      row 16 on wave 1 (per-lane rows: conv0_window).  Each lane stores its
+  //      pixel's 16-B half (see the swizzle): fragment a's in quads 0 and 2,
+  //      b's in quads 1 and 3.
   {
     C0Wts<1> Wt;
     Wt.load(q0, 16, col, quad);
-    auto win = [&](int t, int yr, int j, bool& ok) {
-      const int xr = j < kStXE ? 2 * j : 2 * (j - kStXE) + 1;
-      const int Y = xy0 + yr, X = xx0 + xr;
-      ok = t < kStNpx && (unsigned)Y < (unsigned)H0 && (unsigned)X < (unsigned)W0;
-      return conv0_window(r, Y, X, quad, H, W * 3, ok);
+    const int rowb = W * 3;
+    const int jl = (wave < 2 ? 16 * wave : kStXE + 16 * (wave - 2)) + col;  // stored column
+    const int X = xx0 + (wave < 2 ? 2 * jl : 2 * (jl - kStXE) + 1);
+    const bool xin = (unsigned)X < (unsigned)W0;
+    const int start = 6 * X - 3;
+    const int sh = start & 3;
+    const uint32_t vl = (uint32_t)(quad * rowb + start - sh);  // + (2 Y - 1) rowb
+    const bool lq = xin && quad < 3, lx = X > 0;
+    // the window of strip pixel (Y, X), Y wave-uniform (conv0_window's bytes)
+    auto strip_win = [&](int Y) {
+      C0Win w;
+      w.sh = sh;
+      const bool ok = lq && (unsigned)Y < (unsigned)H0 && (unsigned)(2 * Y - 1 + quad) < (unsigned)H;
+      const uint32_t vb = ok ? vl + (uint32_t)((2 * Y - 1) * rowb) : kOOB;
+      w.w0 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)(lx ? vb : kOOB), 0, 0);
+      w.w1 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)(vb + 4u), 0, 0);
+      w.w2 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)(vb + 8u), 0, 0);
+      return w;
     };
-    // t += 128: 2 rows down, 2 stored columns left (65 = one row)
-    auto adv = [](int& yr, int& j) {
-      j -= 2;
-      yr += 2;
-      if (j < 0) {
-        j += kStXW;
-        yr -= 1;
-      }
-    };
-    int t = 16 * wave + col;
-    int ya = t / kStXW, ja = t - ya * kStXW;
-    int yb = (t + 64) / kStXW, jb = t + 64 - yb * kStXW;
-    const int npairs = (kStNfr - wave + 7) / 8;
-    bool oka, okb;
-    C0Win na = win(t, ya, ja, oka), nb = win(t + 64, yb, jb, okb);
-    for (int i = 0; i < npairs; ++i) {
+    // pair 8's b fragment: wave 0 rows 0-15, wave 1 row 16 (lane 0)
+    const int ye = wave == 0 ? col : kStXR - 1;
+    const int Ye = xy0 + ye, Xe = xx0 + 2 * (kStXE - 1);
+    const bool ve = wave == 0 || (wave == 1 && col == 0);
+    const bool ine = ve && (unsigned)Ye < (unsigned)H0 && (unsigned)Xe < (unsigned)W0;
+    // store address of this lane's pixel in pair 0 (+ 2 rows per pair);
+    // bit 2 of a stored slot is bit 2 of its column (72 = 0 mod 8)
+    const int sbase = ((quad & 1) * kStXS + jl) * 32 + (((quad >> 1) ^ ((jl >> 2) & 1)) << 4);
+    const int se = (ye * kStXS + kStXE - 1) * 32 + ((quad >> 1) << 4);
+    C0Win na = strip_win(xy0), nb = strip_win(xy0 + 1);
+#pragma unroll
+    for (int i = 0; i < (kStXR + 1) / 2; ++i) {
       const C0Win ca = na, cb = nb;
-      const bool cka = oka, ckb = okb;
-      // the pixel this lane stores: fragment f (quads 0, 2) or f + 4 (quads 1, 3)
-      const bool odd = quad & 1;
-      const int ts = odd ? t + 64 : t;
-      const int ss = (odd ? yb : ya) * kStXS + (odd ? jb : ja);
-      if (i + 1 < npairs) {
-        t += 128;
-        adv(ya, ja);
-        adv(yb, jb);
-        na = win(t, ya, ja, oka);
-        nb = win(t + 64, yb, jb, okb);
+      const bool last = 2 * i + 1 == kStXR;
+      const int Ya = xy0 + 2 * i;
+      const bool cka = xin && (unsigned)Ya < (unsigned)H0;
+      const bool ckb = last ? ine : xin && (unsigned)(Ya + 1) < (unsigned)H0;
+      if (2 * i + 3 < kStXR) {
+        na = strip_win(Ya + 2);
+        nb = strip_win(Ya + 3);
+      } else if (2 * i + 3 == kStXR) {
+        na = strip_win(Ya + 2);
+        nb = conv0_window(r, Ye, Xe, quad, H, rowb, ine);
       }
       f32x4 va[1], vb[1];
       conv0_frag<1>(Wt, conv0_bop(ca), va);
@@ -303,9 +321,13 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
       // holds channels 8 (q >> 1) .. +7 of its pixel in (a0, a1, b0, b1)
       const auto x0v = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
       const auto x1v = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
-      if (ts < kStNpx) {
-        const int h = (quad >> 1) ^ ((ss >> 2) & 1);
-        *(uint4*)(xs + ss * 32 + h * 16) = make_uint4(x0v[0], x1v[0], x0v[1], x1v[1]);
+      const uint4 px = make_uint4(x0v[0], x1v[0], x0v[1], x1v[1]);
+      if (!last) {
+        *(uint4*)(xs + sbase + i * 2 * kStRowB) = px;
+      } else if (!(quad & 1)) {
+        *(uint4*)(xs + sbase + i * 2 * kStRowB) = px;
+      } else if (ve) {
+        *(uint4*)(xs + se) = px;
       }
     }
   }
