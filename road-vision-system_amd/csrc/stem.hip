@@ -274,13 +274,16 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
     const int sh = start & 3;
     const uint32_t vl = (uint32_t)(quad * rowb + start - sh);  // + (2 Y - 1) rowb
     const bool lq = xin && quad < 3, lx = X > 0;
+    // out of range for every window dword (+ 0, 4, 8: no 32-bit wrap) and an
+    // inline constant (-16), unlike kOOB, which costs a v_bfrev per select
+    constexpr uint32_t kOOBi = 0xFFFFFFF0u;
     // the window of strip pixel (Y, X), Y wave-uniform (conv0_window's bytes)
     auto strip_win = [&](int Y) {
       C0Win w;
       w.sh = sh;
       const bool ok = lq && (unsigned)Y < (unsigned)H0 && (unsigned)(2 * Y - 1 + quad) < (unsigned)H;
-      const uint32_t vb = ok ? vl + (uint32_t)((2 * Y - 1) * rowb) : kOOB;
-      w.w0 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)(lx ? vb : kOOB), 0, 0);
+      const uint32_t vb = ok ? vl + (uint32_t)((2 * Y - 1) * rowb) : kOOBi;
+      w.w0 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)(lx ? vb : kOOBi), 0, 0);
       w.w1 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)(vb + 4u), 0, 0);
       w.w2 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)(vb + 8u), 0, 0);
       return w;
@@ -402,13 +405,16 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
       x1[n][4 * m + 3] = __builtin_bit_cast(__bf16, (uint16_t)(hi >> 16));
     }
   }
+  // this lane's first X1 pixel (fragment n: + (n >> 1) rows, + 16 (n & 1)
+  // columns; the row / column steps are wave-uniform)
+  const int oyl = oy0 + 2 * wave, oxl = ox0 + col;
+  const size_t pix0 = ((size_t)b * H1 + oyl) * W1 + oxl;
   if (out) {  // X1 (bf16 NHWC, channel stride out_cs)
+    uint16_t* o0 = out + pix0 * out_cs + 8 * quad;
 #pragma unroll
     for (int n = 0; n < NR; ++n) {
-      const int oy = oy0 + 2 * wave + (n >> 1), ox = ox0 + (n & 1) * 16 + col;
-      if (oy >= H1 || ox >= W1) continue;
-      *(uint4*)(out + (((size_t)b * H1 + oy) * W1 + ox) * out_cs + 8 * quad) =
-          __builtin_bit_cast(uint4, x1[n]);
+      if (oyl + (n >> 1) >= H1 || oxl + (n & 1) * 16 >= W1) continue;
+      *(uint4*)(o0 + ((n >> 1) * W1 + (n & 1) * 16) * out_cs) = __builtin_bit_cast(uint4, x1[n]);
     }
   }
   if (out2) {  // the fused 1x1 conv (32 -> 32) from the registers
@@ -419,15 +425,15 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
       A2[m] = __builtin_bit_cast(bf16x8, *(const uint4*)(w2 + (m * 16 + col) * 32 + quad * 8));
       bb2[m] = *(const f32x4*)(b2 + m * 16 + quad * 4);
     }
+    uint16_t* const o0 = out2 + pix0 * out2_cs + (quad & 1) * 16 + (quad >> 1) * 8;
 #pragma unroll
     for (int n = 0; n < NR; ++n) {
-      const int oy = oy0 + 2 * wave + (n >> 1), ox = ox0 + (n & 1) * 16 + col;
       f32x4 d[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m)
         d[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2[m], x1[n], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      if (oy >= H1 || ox >= W1) continue;
-      uint16_t* o = out2 + (((size_t)b * H1 + oy) * W1 + ox) * out2_cs;
+      if (oyl + (n >> 1) >= H1 || oxl + (n & 1) * 16 >= W1) continue;
+      uint16_t* o = o0 + ((n >> 1) * W1 + (n & 1) * 16) * out2_cs;
       // the two fragments as one 16-B store per lane: after the swap quad q
       // holds channels 8 (q >> 1) .. +7 of fragment q & 1 (as conv0 above)
       uint32_t pk[2][2];
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
       }
       const auto y0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
       const auto y1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
-      *(uint4*)(o + (quad & 1) * 16 + (quad >> 1) * 8) = make_uint4(y0[0], y1[0], y0[1], y1[1]);
+      *(uint4*)o = make_uint4(y0[0], y1[0], y0[1], y1[1]);
     }
   }
 }
