@@ -913,7 +913,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
       const int iy = iy0 + (gg & 4095), ix = ix0 + ((gg >> 12) & 4095);
       const bool ok = (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
       // branchless select: an out-of-image slot reads zeros (kOOB)
-      const uint32_t off = (uint32_t)(iy * a.Win + ix) * (uint32_t)pix_bytes + ((gg >> 24) & 3) * 16;
+      // 24-bit multiplies (full rate): a map pixel index and the pixel
+      // stride are < 2^24 and the in-image byte offset < 2^31, so the low 32
+      // bits are the product (an out-of-image slot's garbage is masked)
+      const uint32_t off = __umul24((uint32_t)(__umul24(iy, a.Win) + ix), (uint32_t)pix_bytes) +
+                           ((gg >> 24) & 3) * 16;
       const uint32_t m = ok ? 0u : 0xFFFFFFFFu;
       voff[it] = (off & ~m) | (kOOB & m);
     }
@@ -1338,9 +1342,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_patch_kernel(Co
       for (int n = 0; n < NR; ++n) opx[n] = (uint32_t)((b * a.Ho + py[n]) * a.Wo + px[n]);
       chain_tile(pv, opx);
     } else if (g.fast) {
-      uint32_t opx[NR];
+      uint32_t opx[NR];  // < 2^23 (epi_fast): 24-bit multiplies
 #pragma unroll
-      for (int n = 0; n < NR; ++n) opx[n] = (uint32_t)((b * a.Ho + py[n]) * a.Wo + px[n]);
+      for (int n = 0; n < NR; ++n) opx[n] = __umul24((uint32_t)(b * a.Ho + py[n]), (uint32_t)a.Wo) + px[n];
       f32x4 bl[MR];
       bias_tile(bl);
       if constexpr (kDefer) {
@@ -1573,6 +1577,8 @@ static int conv_nch(const ConvArgs& a) {
 
 static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& smem) {
   if (!((a.k == 1 || a.k == 3) && (a.stride == 1 || a.stride == 2) && a.pad == a.k / 2)) return false;
+  // the kernel's patch offsets use 24-bit multiplies (prep_tile)
+  if ((size_t)a.Hin * a.Win >= (1u << 24) || (size_t)a.in_cs * 2 >= (1u << 24)) return false;
   const int NR = c.nr, MR = c.mr;
   const int NW = c.kind == 2 ? 8 : 4;  // waves per workgroup
   const int P = 16 * NR * NW;
