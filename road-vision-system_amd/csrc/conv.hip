@@ -1487,83 +1487,116 @@ __global__ __launch_bounds__(256, 2) void conv1x1_direct_kernel(ConvArgs a, int 
   // generic epilogue (integer divisions are long VALU sequences)
   const bool need_geo = a.in_up || !fast;
   const TileWalk walk = tile_walk(ntiles);
-  for (int t = walk.t0; t < walk.end; t += walk.step) {
+  // a tile's lane pixels: source pointers of both input views and validity
+  struct Geo {
     const bf16_t* src[NR];
     const bf16_t* src2[NR];
     bool pv[NR];
     int pb[NR], py[NR], px[NR];
+  };
+  auto geo = [&](int t, Geo& G) {
 #pragma unroll
     for (int n = 0; n < NR; ++n) {
       const int p = t * 64 * NR + wave * 16 * NR + n * 16 + col;
-      pv[n] = p < npix;
-      const int pp = pv[n] ? p : 0;
-      pb[n] = py[n] = px[n] = 0;
+      G.pv[n] = t < walk.end && p < npix;
+      const int pp = G.pv[n] ? p : 0;
+      G.pb[n] = G.py[n] = G.px[n] = 0;
       if (need_geo) {
-        pb[n] = pp / HW;
-        const int r = pp - pb[n] * HW;
-        py[n] = r / a.Wo;
-        px[n] = r - py[n] * a.Wo;
+        G.pb[n] = pp / HW;
+        const int r = pp - G.pb[n] * HW;
+        G.py[n] = r / a.Wo;
+        G.px[n] = r - G.py[n] * a.Wo;
       }
       // the `in` view's pixel: itself, or (y/2, x/2) of the half-resolution map
-      const size_t ps = a.in_up ? ((size_t)pb[n] * (a.Ho >> 1) + (py[n] >> 1)) * (a.Wo >> 1) + (px[n] >> 1)
+      const size_t ps = a.in_up ? ((size_t)G.pb[n] * (a.Ho >> 1) + (G.py[n] >> 1)) * (a.Wo >> 1) +
+                                      (G.px[n] >> 1)
                                 : (size_t)pp;
-      src[n] = a.in + ps * a.in_cs + a.in_co + quad * 8;
+      G.src[n] = a.in + ps * a.in_cs + a.in_co + quad * 8;
       // the in2 view, addressed by logical channel (chunks at or above split)
-      src2[n] = a.in2 + (size_t)pp * a.in2_cs + a.in2_co + quad * 8 - a.split;
+      G.src2[n] = a.in2 + (size_t)pp * a.in2_cs + a.in2_co + quad * 8 - a.split;
     }
-    // unconditional loads (invalid pixels / channels read the zero block):
-    // a branch around a load would make the compiler drain vmcnt to 0 before
-    // the MFMAs, i.e. wait for the prefetched chunk as well
-    auto load = [&](int c, uint4 (&B)[NR]) {
-      const bool kin = c * 32 + quad * 8 < a.Cin;
-      const bool second = a.split > 0 && c * 32 >= a.split;
+  };
+  // the B fragments of chunk c of tile G (unconditional loads: invalid
+  // pixels / channels read the zero block; a branch around a load would make
+  // the compiler drain vmcnt to 0 before the MFMAs, i.e. wait for the
+  // prefetched chunks as well)
+  auto load = [&](const Geo& G, int c, uint4 (&B)[NR]) {
+    const bool kin = c * 32 + quad * 8 < a.Cin;
+    const bool second = a.split > 0 && c * 32 >= a.split;
+#pragma unroll
+    for (int n = 0; n < NR; ++n)
+      B[n] = *(const uint4*)((G.pv[n] && kin) ? (const void*)((second ? G.src2[n] : G.src[n]) + c * 32)
+                                              : (const void*)g_zero16);
+  };
+  auto mma = [&](int c, const uint4 (&B)[NR], f32x4 (&acc)[MR][NR]) {
+    const uint8_t* Wl = smem + c * W_BYTES;
+    bf16x8 A[MR];
+#pragma unroll
+    for (int m = 0; m < MR; ++m) A[m] = __builtin_bit_cast(bf16x8, *(const uint4*)(Wl + aoff[m]));
+    // all MR weight reads in flight before the first MFMA (left alone, the
+    // scheduler waits for each A fragment right before its MFMAs)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
 #pragma unroll
       for (int n = 0; n < NR; ++n)
-        B[n] = *(const uint4*)((pv[n] && kin) ? (const void*)((second ? src2[n] : src[n]) + c * 32)
-                                              : (const void*)g_zero16);
-    };
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[m], __builtin_bit_cast(bf16x8, B[n]),
+                                                            acc[m][n], 0, 0, 0);
+  };
+  auto finish = [&](int t, const Geo& G, f32x4 (&acc)[MR][NR]) {
+    if (fast) {
+      uint32_t opx[NR];
+#pragma unroll
+      for (int n = 0; n < NR; ++n) opx[n] = (uint32_t)(t * 64 * NR + wave * 16 * NR + n * 16 + col);
+      epilogue_fast<MR, NR>(a, acc, cout0, G.pv, opx, quad, bias);
+    } else {
+      epilogue<MR, NR>(a, acc, cout0, G.pv, G.pb, G.py, G.px, quad, bias);
+    }
+  };
+  // A stream of (tile, chunk) positions with two chunk loads always in
+  // flight ACROSS tile boundaries: the last chunks' MFMAs and the epilogue of
+  // tile t run while tile t + step's first two chunks load (G1), so a
+  // persistent block never restarts its pipeline from an empty queue, and no
+  // chunk is loaded twice.  A tile spans P = nch rounded up to even positions
+  // (an odd count's last position reads the zero block: the k-order and sums
+  // are unchanged).
+  const int P = (nch + 1) & ~1;
+  uint4 B0[NR], B1[NR];
+  Geo G0, G1;
+  int t = walk.t0;
+  geo(t, G0);
+  geo(t + walk.step, G1);
+  // (the last pair of positions is peeled: no branch around a load, which
+  // made the compiler wait for every outstanding load at the join)
+  load(G0, 0, B0);
+  load(G0, 1, B1);
+  for (; t < walk.end; t += walk.step) {
     f32x4 acc[MR][NR];
 #pragma unroll
     for (int m = 0; m < MR; ++m)
 #pragma unroll
       for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto mma = [&](int c, const uint4 (&B)[NR]) {
-      const uint8_t* Wl = smem + c * W_BYTES;
-      bf16x8 A[MR];
-#pragma unroll
-      for (int m = 0; m < MR; ++m) A[m] = __builtin_bit_cast(bf16x8, *(const uint4*)(Wl + aoff[m]));
-      // all MR weight reads in flight before the first MFMA (left alone, the
-      // scheduler waits for each A fragment right before its MFMAs)
+    for (int c = 0; c < P - 2; c += 2) {  // B0: chunk c, B1: chunk c + 1 (< nch here)
+      mma(c, B0, acc);
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int m = 0; m < MR; ++m)
-#pragma unroll
-        for (int n = 0; n < NR; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[m], __builtin_bit_cast(bf16x8, B[n]),
-                                                              acc[m][n], 0, 0, 0);
-    };
-    // ping-pong register buffers, chunk c+1 in flight during chunk c's MFMAs
-    // (indices clamped instead of branched, so the loads stay countable)
-    uint4 B0[NR], B1[NR];
-    load(0, B0);
-    for (int c = 0; c < nch; c += 2) {
-      load(c + 1 < nch ? c + 1 : nch - 1, B1);
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs
-      mma(c, B0);
+      load(G0, c + 2, B0);
       __builtin_amdgcn_sched_barrier(0);
-      load(c + 2 < nch ? c + 2 : nch - 1, B0);
+      mma(c + 1, B1, acc);
       __builtin_amdgcn_sched_barrier(0);
-      if (c + 1 < nch) mma(c + 1, B1);
+      load(G0, c + 3, B1);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (fast) {
-      uint32_t opx[NR];
-#pragma unroll
-      for (int n = 0; n < NR; ++n) opx[n] = (uint32_t)(t * 64 * NR + wave * 16 * NR + n * 16 + col);
-      epilogue_fast<MR, NR>(a, acc, cout0, pv, opx, quad, bias);
-    } else {
-      epilogue<MR, NR>(a, acc, cout0, pv, pb, py, px, quad, bias);
-    }
+    mma(P - 2, B0, acc);
+    __builtin_amdgcn_sched_barrier(0);
+    load(G1, 0, B0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (P - 1 < nch) mma(P - 1, B1, acc);  // odd nch: position P - 1 is padding
+    __builtin_amdgcn_sched_barrier(0);
+    load(G1, 1, B1);
+    __builtin_amdgcn_sched_barrier(0);
+    finish(t, G0, acc);
+    G0 = G1;
+    geo(t + 2 * walk.step, G1);
   }
 }
 
