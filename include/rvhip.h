@@ -192,6 +192,12 @@ int rv_yolo_destroy(void* handle);
  * forwards (raw_out) keep the decode kernel.  Off by default: on MI355X the
  * chained 3x3 launches cost what the decode saves. */
 #define RV_YOLO_OPT_HEAD_CHAIN 6
+/* RV_YOLO_OPT_C2F_TAP_PAIRS (default 1): the fused hidden-width-16 C2f chain
+ * (model.2 of YOLOv8n) runs its 3x3 convs on tap pairs -- two taps' 16
+ * channels per 32-deep MFMA k-step, 5 k-steps instead of 9 half-zero ones;
+ * the sums round differently (within 1 bf16 ulp of the per-tap order).
+ * 0: the per-tap k order, bit-identical to the unfused launches. */
+#define RV_YOLO_OPT_C2F_TAP_PAIRS 7
 int rv_yolo_set_option(void* handle, int opt, int value);
 
 /* fp8 plans (BASELINE configs[4]: "YOLOv8m 1280x1280 fp8 MFMA conv path").

@@ -84,7 +84,7 @@ __device__ __forceinline__ void c2f_conv3(const uint8_t* __restrict__ in, uint8_
                                           const bf16_t* __restrict__ w,
                                           const float* __restrict__ bias,
                                           const uint8_t* __restrict__ res, int oy0, int ox0, int H,
-                                          int W, const uint8_t* __restrict__ zeros) {
+                                          int W, const uint8_t* __restrict__ zeros, bool pairs) {
   using G = C2fGeo<C>;
   using T = C2fTile<TR, TC>;
   constexpr int MR = G::MR;
@@ -104,6 +104,82 @@ __device__ __forceinline__ void c2f_conv3(const uint8_t* __restrict__ in, uint8_
 #pragma unroll
   for (int m = 0; m < MR; ++m) bv[m] = *(const f32x4c*)(bias + m * 16 + quad * 4);
   const int nfrag = (rpo + 15) / 16;
+  if (C == 16 && pairs) {  // block-uniform
+    // Tap pairs (the stem's model.1 form): a 32-deep k-step takes the 16
+    // channels of two taps -- quads 0, 1 tap 2p, quads 2, 3 tap 2p + 1 (the
+    // last, tap 8, pairs with zero weights) -- so a 16-channel 3x3 conv is 5
+    // MFMAs and 5 B reads per fragment instead of 9 half-zero ones.  The sums
+    // differ from the unfused per-tap k-steps by rounding only (1 bf16 ulp:
+    // tests/test_yolo_layers_gpu.py).  Pair p's second tap is tap 2p + 1:
+    // the next pixel for p = 0, 2, 3, the next row's first for p = 1.
+    bf16x8c Ap[5];
+#pragma unroll
+    for (int p = 0; p < 5; ++p) {
+      const int t = 2 * p + (quad >> 1);
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (t < 9) v = *(const uint4*)(w + ((size_t)col * 9 + t) * 32 + (quad & 1) * 8);
+      Ap[p] = __builtin_bit_cast(bf16x8c, v);
+    }
+    const bool hiq = quad >= 2;
+    for (int f0 = wave * 2; f0 < nfrag; f0 += 16) {
+      f32x4c acc[2];
+      int o[2];
+      const uint8_t* b1[2];  // pairs 0, 2, 3: tap 2p + (quad >> 1)
+      const uint8_t* b2[2];  // pair 1: taps 2 (0, 2) and 3 (1, 0)
+      const uint8_t* b4[2];  // tap 8 (quads 0, 1) or zeros
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        o[n] = (f0 + n) * 16 + col;
+        const int oo = o[n] < rpo ? o[n] : 0;
+        const int r = oo / rwo, c = oo - r * rwo;
+        const uint8_t* bp = in + G::addr(r * rwi + c, quad & 1);
+        b1[n] = bp + (hiq ? G::PB : 0);
+        b2[n] = bp + (hiq ? (rwi - 2) * G::PB : 0) + (2 * G::PB);
+        b4[n] = hiq ? zeros : bp + (2 * rwi + 2) * G::PB;
+        acc[n] = f32x4c{0.f, 0.f, 0.f, 0.f};
+      }
+      bf16x8c Bp[5][2];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        Bp[0][n] = __builtin_bit_cast(bf16x8c, *(const uint4*)(b1[n]));
+        Bp[1][n] = __builtin_bit_cast(bf16x8c, *(const uint4*)(b2[n]));
+        Bp[2][n] = __builtin_bit_cast(bf16x8c, *(const uint4*)(b1[n] + (rwi + 1) * G::PB));
+        Bp[3][n] = __builtin_bit_cast(bf16x8c, *(const uint4*)(b1[n] + (2 * rwi) * G::PB));
+        Bp[4][n] = __builtin_bit_cast(bf16x8c, *(const uint4*)(b4[n]));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < 5; ++p)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ap[p], Bp[p][n], acc[n], 0, 0, 0);
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        if (o[n] >= rpo) continue;
+        const int r = o[n] / rwo, c = o[n] - (o[n] / rwo) * rwo;
+        const int gy = oy0 - e_out + r, gx = ox0 - e_out + c;
+        const bool inside = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = acc[n][i] + bv[0][i];
+        silu4(v);
+        const int lq = (quad * 4) >> 3, half = (quad & 1) * 8;
+        if (RES) {
+          const int d = e_res - e_out;
+          const int pr = (r + d) * rwr + c + d;
+          const uint2 rr = *(const uint2*)(res + G::addr(pr, lq) + half);
+          v[0] += c2f_bf2f(rr.x & 0xFFFF);
+          v[1] += c2f_bf2f(rr.x >> 16);
+          v[2] += c2f_bf2f(rr.y & 0xFFFF);
+          v[3] += c2f_bf2f(rr.y >> 16);
+        }
+        const uint2 pk = inside ? make_uint2(c2f_pack(v[0], v[1]), c2f_pack(v[2], v[3]))
+                                : make_uint2(0, 0);
+        *(uint2*)(outb + G::addr(o[n], lq) + half) = pk;
+      }
+    }
+    return;
+  }
   for (int f0 = wave * 2; f0 < nfrag; f0 += 16) {
     f32x4c acc[2][MR];
     int o[2];
@@ -229,17 +305,17 @@ __global__ __launch_bounds__(512) void c2f_chain_kernel(C2fArgs a) {
   // ---- 2. bottlenecks: t = cva(y_in) at halo e-1, z = [y_in +] cvb(t) at e-2
   const uint8_t* zeros = smem + L::ZR;
   c2f_conv3<C, TR, TC, false, h - 1, 0>(smem + L::Y, smem + L::Tb, a.wa[0], a.ba[0], nullptr, oy0,
-                                        ox0, a.H, a.W, zeros);
+                                        ox0, a.H, a.W, zeros, a.tap_pairs != 0);
   __syncthreads();
   c2f_conv3<C, TR, TC, SC, h - 2, h>(smem + L::Tb, smem + L::Z0, a.wb[0], a.bb[0], smem + L::Y, oy0,
-                                     ox0, a.H, a.W, zeros);
+                                     ox0, a.H, a.W, zeros, a.tap_pairs != 0);
   __syncthreads();
   if constexpr (N == 2) {
     c2f_conv3<C, TR, TC, false, h - 3, 0>(smem + L::Z0, smem + L::Tb, a.wa[1], a.ba[1], nullptr, oy0,
-                                          ox0, a.H, a.W, zeros);
+                                          ox0, a.H, a.W, zeros, a.tap_pairs != 0);
     __syncthreads();
     c2f_conv3<C, TR, TC, SC, h - 4, h - 2>(smem + L::Tb, smem + L::Z1, a.wb[1], a.bb[1],
-                                           smem + L::Z0, oy0, ox0, a.H, a.W, zeros);
+                                           smem + L::Z0, oy0, ox0, a.H, a.W, zeros, a.tap_pairs != 0);
     __syncthreads();
   }
 

@@ -126,7 +126,8 @@ int launch_sppf_pool_fp8(uint8_t* buf, int B, int H, int W, int c, hipStream_t s
 // width C in {16, 32} and N in {1, 2} bottlenecks (C = 16: N = 1): reads
 // y0 / y1 (cv1's output, channels [cat_co, cat_co + 2C) of the block's
 // concat buffer), writes cv2's 2C channels to the output view.  Every
-// intermediate stays in LDS.  Bit-identical to the unfused launches.
+// intermediate stays in LDS.  Bit-identical to the unfused launches (C = 16
+// with tap_pairs: within 1 bf16 ulp).
 struct C2fArgs {
   const bf16_t* cat;
   int cat_cs, cat_co;
@@ -139,6 +140,10 @@ struct C2fArgs {
   const float* b2;
   bf16_t* out;
   int out_cs, out_co;
+  // C = 16: the 3x3 convs on tap pairs (two taps' 16 channels per 32-deep
+  // k-step; within 1 bf16 ulp of the per-tap k order) instead of one
+  // half-zero k-step per tap (bit-identical to the unfused launches)
+  int tap_pairs;
 };
 bool c2f_fusable(int C, int N, int cat_cs, int cat_co, int out_cs, int out_co);
 int launch_c2f_chain(const C2fArgs& a, int C, int N, bool shortcut, hipStream_t s);

@@ -346,6 +346,7 @@ struct Model {
   int head_streams = 1;            // RV_YOLO_OPT_HEAD_STREAMS
   int fuse_cv1 = 1;                // RV_YOLO_OPT_FUSE_CV1
   int head_chain = 0;              // RV_YOLO_OPT_HEAD_CHAIN (measured neutral: DESIGN.md)
+  int c2f_tap_pairs = 1;           // RV_YOLO_OPT_C2F_TAP_PAIRS
   std::vector<Buf> bufs;
   int nA = 0;
   int map_h[6], map_w[6];  // stride 2^i maps
@@ -764,6 +765,7 @@ struct Exec {
       f.a.H = M->map_h[li];
       f.a.W = M->map_w[li];
       f.a.B = B;
+      f.a.tap_pairs = M->c2f_tap_pairs;
       double flops = 0.0;
       ConvArgs rec;
       for (int i = 0; i < n; ++i) {
@@ -1021,6 +1023,9 @@ extern "C" int rv_yolo_set_option(void* h, int opt, int value) {
       return RV_OK;
     case RV_YOLO_OPT_HEAD_CHAIN:
       M->head_chain = value != 0;
+      return RV_OK;
+    case RV_YOLO_OPT_C2F_TAP_PAIRS:
+      M->c2f_tap_pairs = value != 0;
       return RV_OK;
     default:
       set_error("unknown yolo option %d", opt);

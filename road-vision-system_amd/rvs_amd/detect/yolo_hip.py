@@ -221,11 +221,19 @@ class YoloEngine:
 
     def set_head_chain(self, on: bool) -> None:
         """Candidate forwards run each Detect branch's last 1x1 conv inside
-        its 3x3 conv's launch plus one small combine kernel (True, default)
+        its 3x3 conv's launch plus one small combine kernel (True)
         or through the decode kernel (RV_YOLO_OPT_HEAD_CHAIN; the same
-        candidates)."""
+        candidates; off by default)."""
         for h in self._hs:
             call("rv_yolo_set_option", h, 6, 1 if on else 0)
+
+    def set_c2f_tap_pairs(self, on: bool) -> None:
+        """The fused width-16 C2f chain's 3x3 convs on tap pairs (True,
+        default: within 1 bf16 ulp of the per-tap k order) or one k-step per
+        tap (False: bit-identical to the unfused launches;
+        RV_YOLO_OPT_C2F_TAP_PAIRS)."""
+        for h in self._hs:
+            call("rv_yolo_set_option", h, 7, 1 if on else 0)
 
     def set_fuse_c2f(self, on) -> None:
         """Narrow C2f blocks as one fused launch or one launch per conv

@@ -302,13 +302,15 @@ def test_fused_c2f_is_bit_identical(cuda, H, W, B, variant):
     + cv2 in one launch each, intermediates in LDS) against one launch per
     conv, on the production kernel sequence: every output map of the blocks,
     the raw prediction and the NMS candidates are bit-identical (same MFMA
-    k-order and epilogue)."""
+    k-order and epilogue; the width-16 chain with its per-tap k-steps,
+    RV_YOLO_OPT_C2F_TAP_PAIRS = 0)."""
     from rvs_amd.detect import weights
     from rvs_amd.detect.yolo_hip import YoloEngine
     eng = YoloEngine(variant, weights.synthetic_weights(variant, seed=5), B, (H, W), device=cuda)
     fr = np.stack([cpu.median(cpu.clahe_ycrcb(road_frame(H, W, seed=90 + b)), 3) for b in range(B)])
     lb = eng.letterbox(torch.from_numpy(fr).to(cuda))
     eng.set_raw_fused(True)
+    eng.set_c2f_tap_pairs(False)
     outs = []
     for fuse in (False, True):
         eng.set_fuse_c2f(2 if fuse else 0)  # every fusable chain (the default fuses C = 16 only)
@@ -332,6 +334,50 @@ def test_fused_c2f_is_bit_identical(cuda, H, W, B, variant):
         np.testing.assert_array_equal(m1[k], m0[k], err_msg=k)
     np.testing.assert_array_equal(r1, r0)
     np.testing.assert_array_equal(s1, s0)
+    eng.close()
+
+
+@pytest.mark.parametrize("H,W,B", [(1080, 1920, 3), (640, 640, 1), (360, 640, 2)])
+def test_c2f_tap_pairs_within_one_ulp(cuda, H, W, B):
+    """The production width-16 C2f chain (model.2: its 3x3 convs on tap
+    pairs, two taps' 16 channels per 32-deep MFMA k-step) against the
+    per-tap k order (bit-identical to the unfused launches): the block's
+    output X2 agrees to 1 bf16 ulp (fewer than 1e-3 of the elements beyond,
+    none beyond 2 ulp + 1e-2 rms -- the stem's model.1 bar), and the
+    forward's candidates per image stay within 1 % of each other.  (On
+    MI355X the two k orders have agreed bit for bit on every input measured:
+    the zero upper k-half of a per-tap step adds nothing, so both add the
+    same products in the same k order; the bar stays at 1 ulp.)"""
+    from rvs_amd.detect import weights
+    from rvs_amd.detect.yolo_hip import YoloEngine
+    eng = YoloEngine(0, weights.synthetic_weights(0, seed=5), B, (H, W), device=cuda)
+    fr = np.stack([cpu.median(cpu.clahe_ycrcb(road_frame(H, W, seed=95 + b)), 3) for b in range(B)])
+    lb = eng.letterbox(torch.from_numpy(fr).to(cuda))
+    eng.set_raw_fused(True)
+    outs = []
+    for pairs in (False, True):
+        eng.set_c2f_tap_pairs(pairs)
+        raw = torch.empty((B, 84, eng.A), dtype=torch.float32, device=cuda)
+        eng.forward_raw(lb, raw, slot=int(pairs))
+        torch.cuda.synchronize()
+        ins = Introspect(eng, B)
+        specs, _ = yolo_ref.conv_specs(0)
+        x2 = None
+        for rec in ins.recs:
+            if specs[rec[0]][0] == "model.2.cv2":
+                x2 = ins.view(rec[8])[..., rec[10]:rec[10] + specs[rec[0]][2]].copy()
+        nseg = eng.nseg
+        seg = eng.seg_n[int(pairs)].view(-1)[:B * nseg].view(B, nseg).cpu().numpy().copy()
+        outs.append((x2, raw.cpu().numpy(), seg))
+    (x0, r0, s0), (x1, r1, s1) = outs
+    assert x0 is not None and x0.shape == x1.shape
+    rms = float(np.sqrt(np.mean(x0.astype(np.float64) ** 2))) + 1e-12
+    d = np.abs(x1.astype(np.float64) - x0)
+    assert float((d > ulp_bf16(x0) * 1.01 + 1e-3 * rms).mean()) < 1e-3
+    assert (d <= 2 * ulp_bf16(x0) + 1e-2 * rms).all()
+    assert np.isfinite(r1).all()
+    n0, n1 = s0.sum(axis=-1), s1.sum(axis=-1)
+    assert (np.abs(n1 - n0) <= 0.01 * np.maximum(n0, 100)).all()
     eng.close()
 
 
