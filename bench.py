@@ -84,10 +84,11 @@ def parse_args(argv=None):
     ap.add_argument("--pair", type=int, default=int(os.environ.get("RV_PAIR", 4)),
                     help="steps per pipeline unit (one forward over pair x streams frames); the "
                          "largest divisor of --steps not above it is used")
-    ap.add_argument("--units", default=os.environ.get("RV_UNITS", "even"),
-                    help="pipeline unit sizes: 'even' (--steps / pair units of pair steps), "
-                         "'ramp' (units of 1 and 2 steps at both ends of the run, pair steps "
-                         "between: a shorter pipeline fill and drain), or an explicit "
+    ap.add_argument("--units", default=os.environ.get("RV_UNITS", "ends"),
+                    help="pipeline unit sizes: 'ends' (default: half units of pair / 2 steps "
+                         "first and last, pair steps between -- at --steps 20, 2,4,4,4,4,2), "
+                         "'even' (--steps / pair units of pair steps), 'ramp' (units of 1 and 2 "
+                         "steps at both ends of the run, pair steps between), or an explicit "
                          "comma-separated list summing to --steps")
     ap.add_argument("--warm-runs", type=int, default=int(os.environ.get("RV_WARM_RUNS", 3)),
                     help="untimed runs of the recorded schedule over the timed frames before the "
@@ -130,7 +131,8 @@ def pick_pair(steps: int, pair: int) -> int:
 
 def unit_sizes(steps: int, pair: int, spec: str) -> list:
     """Steps per pipeline unit, in order (rvs_amd.schedule.PipelinedRun
-    units).  'even': steps / p units of p = pick_pair(steps, pair); 'ramp':
+    units).  'even': steps / p units of p = pick_pair(steps, pair); 'ends':
+    the same with the first and the last unit split in halves; 'ramp':
     1- and 2-step units at both ends (the first unit's preprocess and the
     last unit's forward + tracking run with little beside them, so small end
     units shorten the fill and the drain), units of `pair` between, any
@@ -138,6 +140,16 @@ def unit_sizes(steps: int, pair: int, spec: str) -> list:
     if spec == "even":
         p = pick_pair(steps, pair)
         return [p] * (steps // p)
+    if spec == "ends":
+        # the first unit's preprocess runs with nothing beside it (the fill)
+        # and the last unit's forward + tracking with little beside it (the
+        # drain); half-size units there shorten both (r06: 2,4,4,4,4,2 vs
+        # even at --steps 20, three interleaved rounds on one box: 47.2k vs
+        # 46.5k frames/s, profiles/r06/unit_layout_ab.txt)
+        p = pick_pair(steps, pair)
+        if p % 2 or steps // p < 2:
+            return [p] * (steps // p)
+        return [p // 2] + [p] * (steps // p - 1) + [p // 2]
     if spec == "ramp":
         head = [h for h in (1, 2) if h < pair]
         if 2 * sum(head) + pair > steps:
