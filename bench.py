@@ -52,7 +52,7 @@ PEAK_HBM = 8000.0                      # GB/s
 IMAGE_POINTS = [[560, 1000], [1360, 1000], [1160, 620], [760, 620]]
 WORLD_POINTS = [[-3.5, 5.0], [3.5, 5.0], [3.5, 30.0], [-3.5, 30.0]]
 METRIC = "end-to-end frames/sec @1080p (preproc+YOLOv8n+SORT), 1/2/4/8 MI355X"
-PMC_TRAFFIC = os.path.join(REPO, "profiles", "r05", "pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "r06", "pmc_traffic.json")
 LIB = os.path.join(REPO, "road-vision-system_amd", "rvs_amd", "librvhip.so")
 
 
@@ -485,19 +485,19 @@ def _lib_sha256() -> str:
 
 def pmc_traffic() -> dict:
     """HBM bytes per step of the conv family from rocprofv3 PMC passes
-    (tools/gpu_pmc.sh -> profiles/r05/pmc_traffic.json), reported only when
+    (tools/gpu_pmc.sh -> profiles/r06/pmc_traffic.json), reported only when
     they were collected on the library this run loaded (same sha256)."""
     if not os.path.exists(PMC_TRAFFIC):
         return {"traffic": None, "traffic_note": "no PMC pass of this round's library"}
     d = json.load(open(PMC_TRAFFIC))
     if d.get("librvhip_sha256") != _lib_sha256():
         return {"traffic": None,
-                "traffic_note": "the PMC passes in profiles/r05/pmc_traffic.json were collected "
+                "traffic_note": "the PMC passes in profiles/r06/pmc_traffic.json were collected "
                                 "on another build of librvhip.so: not reported"}
     return {"traffic": d.get("conv_bytes_per_step"),
             "traffic_unit": "HBM bytes per step, all conv launches (rocprofv3 PMC: 2 x "
                             "FETCH_SIZE + WRITE_SIZE, separate passes, this build; "
-                            "profiles/r05/pmc_traffic.json)"}
+                            "profiles/r06/pmc_traffic.json)"}
 
 
 def conv_roofline(job, mode: str) -> dict:
