@@ -478,6 +478,24 @@ def _conv_pass(job, mode: str, tags):
             float(by[valid].sum()) / per, int(valid.sum()) / per, union)
 
 
+def _sort_phase_report():
+    """Per-phase time of the fused SORT kernel averaged over every block of
+    the run (a -DRV_SORT_PHASE build, RV_LIB_VARIANT=sph: tools/sort_phase.py);
+    None for the production build."""
+    from rvs_amd import _lib
+    lib = _lib.load()
+    if not hasattr(lib, "rv_sort_phase_read"):
+        return None
+    import ctypes
+    buf = (ctypes.c_ulonglong * 8)()
+    lib.rv_sort_phase_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.rv_sort_phase_read(buf, 0)
+    n = max(1, buf[7])
+    names = ["predict+load", "iou pairs", "sort", "greedy", "bookkeeping", "kf update+metrics"]
+    return {"blocks": int(buf[7]), **{k: round(buf[i] / n / 100.0, 2) for i, k in enumerate(names)},
+            "unit": "us per block (wall clock, 100 MHz)"}
+
+
 def _lib_sha256() -> str:
     with open(LIB, "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()
@@ -857,6 +875,7 @@ def main(argv=None):
     # the same K steps again without the consumer, from the same SORT state:
     # the device-only rate, and the steady state from its per-step completions
     t2 = rank_job_again(job, dev) if job.consume == "consume" else None
+    sort_phase = _sort_phase_report()
     job.t_device_only = t2["local_s"] if t2 is not None else None
     steady = steady_state(job) if world == 1 else {}
     roof = conv_roofline(job, args.conv_timing) if args.conv_timing != "none" else None
@@ -906,6 +925,8 @@ def main(argv=None):
     }
     res.update(_rank_fields(t, world, dev))
     if t2 is not None:
+        if sort_phase is not None:
+            res["sort_phase"] = sort_phase
         res["device_only"] = {"value": round(t2["value"], 2),
                               "ms_per_step": round(t2["elapsed_s"] / K * 1e3, 4),
                               "note": "the same K steps timed again without the Detection "

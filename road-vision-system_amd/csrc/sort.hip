@@ -36,11 +36,11 @@ struct Track {
   double P[49];
   double t_pred, t_upd;
   double cur_dist, cur_speed;  // NaN = None
-  double hist[kHist][3];       // (t, X, Y)
+  double hist[kHist][3];       // (t, X, Y): a ring, oldest at hist_h
   int id, hits, streak, cls;
   float conf;
-  int hist_n;
-  int pad[4];
+  int hist_n, hist_h;
+  int pad[3];
 };
 static_assert(sizeof(Track) % 16 == 0, "Track alignment");
 
@@ -245,24 +245,35 @@ __device__ void update_metrics(const SortParams& p, Track& t, double x1, double 
     return;
   }
   t.cur_dist = distance(p, X, Y);
-  int n = t.hist_n;
-  t.hist[n][0] = ts;
-  t.hist[n][1] = X;
-  t.hist[n][2] = Y;
+  // the history deque as a ring of kHist entries (at most 32 kept, so the
+  // appended slot never overwrites a live one): appending and dropping move
+  // the two ends only -- shifting the kept entries down after every drop
+  // was a chain of dependent global loads and stores per frame (most of
+  // the fused SORT kernel's update phase)
+  int n = t.hist_n, h = t.hist_h;
+  const int w = h + n < kHist ? h + n : h + n - kHist;
+  t.hist[w][0] = ts;
+  t.hist[w][1] = X;
+  t.hist[w][2] = Y;
   ++n;
   int drop = 0;
   const double win = fmax(0.05, p.speed_window);
-  while (drop < n && (ts - t.hist[drop][0]) > win) ++drop;
+  auto at = [&](int i) -> const double* {  // i-th oldest kept entry
+    const int k = h + i;
+    return t.hist[k < kHist ? k : k - kHist];
+  };
+  while (drop < n && (ts - at(drop)[0]) > win) ++drop;
   if (n - drop > 32) drop = n - 32;
-  if (drop > 0) {
-    for (int i = 0; i < n - drop; ++i)
-      for (int c = 0; c < 3; ++c) t.hist[i][c] = t.hist[i + drop][c];
-    n -= drop;
-  }
+  h += drop;
+  if (h >= kHist) h -= kHist;
+  n -= drop;
   t.hist_n = n;
+  t.hist_h = h;
   if (n >= 2) {
-    const double dt = fmax(1e-3, t.hist[n - 1][0] - t.hist[0][0]);
-    const double dist = hypot(t.hist[n - 1][1] - t.hist[0][1], t.hist[n - 1][2] - t.hist[0][2]);
+    const double* f = at(0);
+    const double* l = at(n - 1);
+    const double dt = fmax(1e-3, l[0] - f[0]);
+    const double dist = hypot(l[1] - f[1], l[2] - f[2]);
     t.cur_speed = dist / dt;
   } else {
     t.cur_speed = NAN;
@@ -283,6 +294,7 @@ __device__ void track_init(Track& t, int id, const float* det, double ts) {
   t.cls = (int)det[5];
   t.conf = det[4];
   t.hist_n = 0;
+  t.hist_h = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -422,6 +434,25 @@ __device__ __forceinline__ void sort_update_row(Track* __restrict__ pool, const 
   }
 }
 
+#ifdef RV_SORT_PHASE
+// timing build (tools/sort_phase.py): per-phase wall-clock ticks (100 MHz)
+// of the fused kernel summed over blocks, read back by rv_sort_phase_read
+__device__ unsigned long long g_sort_phase[8];
+#define RV_PH(i)                                                                       \
+  do {                                                                                 \
+    __syncthreads();                                                                   \
+    if (threadIdx.x == 0) {                                                            \
+      const unsigned long long now = wall_clock64();                                   \
+      atomicAdd(&g_sort_phase[i], now - ph_t);                                         \
+      ph_t = now;                                                                      \
+    }                                                                                  \
+  } while (0)
+#else
+#define RV_PH(i) \
+  do {           \
+  } while (0)
+#endif
+
 // FUSED (rv_sort_update's default, one launch per frame): the block also
 // runs the KF predict of its stream's tracks (sort_predict_kernel's work,
 // boxes and last_update_ts straight into LDS) and, after the bookkeeping,
@@ -460,6 +491,10 @@ __global__ __launch_bounds__(NT) void sort_associate_kernel(
 
   const int s = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
+#ifdef RV_SORT_PHASE
+  unsigned long long ph_t = wall_clock64();
+  if (threadIdx.x == 0) atomicAdd(&g_sort_phase[7], 1ull);  // blocks timed
+#endif
   const StreamHdr h = hdr[s];
   const int T = h.T;
   int D = dcount[s];
@@ -491,6 +526,7 @@ __global__ __launch_bounds__(NT) void sort_associate_kernel(
   }
   if (tid == 0) s_cnt = 0;
   __syncthreads();
+  RV_PH(0);  // predict + loads
 
   // ---- association (_associate, sort_tracker.py:182-210)
   if (T > 0 && D > 0) {
@@ -518,6 +554,7 @@ __global__ __launch_bounds__(NT) void sort_associate_kernel(
       }
     }
     __syncthreads();
+    RV_PH(1);  // IoU pairs
     const int cnt = s_cnt;
     if (cnt <= kKeyCap) {
       int np2 = 1;
@@ -551,6 +588,7 @@ __global__ __launch_bounds__(NT) void sort_associate_kernel(
           }
           __syncthreads();
         }
+      RV_PH(2);  // sort
       // greedy walk in (IoU desc, flat index asc) order, 64 pairs at a time:
       // a pair is accepted iff its row and column are still free; inside a
       // chunk the lowest remaining lane is accepted and the lanes sharing its
@@ -635,6 +673,7 @@ __global__ __launch_bounds__(NT) void sort_associate_kernel(
     }
   }
   __syncthreads();
+  RV_PH(3);  // greedy walk (or the fallback loop)
 
   // ---- bookkeeping (sort_tracker.py:234-276)
   const int n_new = block_rank<NT>([&](int d) { return det_match[d] < 0; }, D, rank_d, wtot);
@@ -699,12 +738,26 @@ __global__ __launch_bounds__(NT) void sort_associate_kernel(
     // sort_update_kernel's work: the streak resets above and the predicted
     // states are this block's own global writes, visible after the barrier
     __syncthreads();
+    RV_PH(4);  // bookkeeping
     double* ap = (double*)smem + tid;
     if (tid < kUpd)
       for (int d = tid; d < p.dmax; d += kUpd)
         sort_update_row(pool, dets, ts, s, d, ljob[d], p, out_id, out_dist, out_speed, ap, kUpd);
+    RV_PH(5);  // KF updates + metrics
   }
 }
+
+#ifdef RV_SORT_PHASE
+extern "C" int rv_sort_phase_read(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort_phase), sizeof(unsigned long long) * 8) != hipSuccess)
+    return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_sort_phase), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 // One thread per detection row of every stream (sort_tracker.py:234-269).
 __global__ __launch_bounds__(kUpdLanes) void sort_update_kernel(
