@@ -198,6 +198,18 @@ int rv_yolo_destroy(void* handle);
  * the sums round differently (within 1 bf16 ulp of the per-tap order).
  * 0: the per-tap k order, bit-identical to the unfused launches. */
 #define RV_YOLO_OPT_C2F_TAP_PAIRS 7
+
+/* One bf16 NHWC conv through the detector's conv launcher (layer tests;
+ * the building block behind rv_yolo_forward, which the reference's
+ * model.predict call replaces, src/detect/yolo_ultralytics.py:28-35):
+ * k in {1, 3} (pad k / 2), stride 1 or 2, bias, SiLU when act != 0, plus an
+ * optional bf16 residual view of the output's shape.  w: packed
+ * [Cout_pad16][k*k][Cin_pad32] bf16, bias: f32 [Cout_pad16].  cfg6
+ * (nullable): {MR, NR, G, resw, persist, kind} as rv_yolo_tuned_config
+ * reports; RV_EINVAL when it is not valid for the layer. */
+int rv_conv_bf16(const void* in, int B, int Hin, int Win, int Cin, int in_cs, const void* w,
+                 const float* bias, int Cout, int k, int stride, void* out, int out_cs,
+                 const void* res, int res_cs, int act, const int* cfg6, void* stream);
 int rv_yolo_set_option(void* handle, int opt, int value);
 
 /* fp8 plans (BASELINE configs[4]: "YOLOv8m 1280x1280 fp8 MFMA conv path").

@@ -283,7 +283,7 @@ __global__ __launch_bounds__(512) void c2f_chain_kernel(C2fArgs a) {
         const int gy = oy0 - e + r, gx = ox0 - e + c;
         if ((unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W)
           // the pixel index (< H * W) widened before the channel-stride multiply
-          v = *(const uint4*)(img + (size_t)(gy * a.W + gx) * a.cat_cs + ch + q * 8);
+          v = *(const uint4*)(img + ((size_t)gy * a.W + gx) * a.cat_cs + ch + q * 8);
       }
       return v;
     };

@@ -2802,4 +2802,49 @@ int launch_detect_decode(const HeadLevel* lv, int nlv, int B, int nc, int reg_ma
   return launch_status("detect_decode");
 }
 
+
+// One bf16 conv (k 1 or 3, pad k / 2, SiLU optional, optional bf16 residual
+// of the output's shape) through the production launcher, for layer tests:
+// the weights packed as yolo.hip packs them ([Cout_pad16][k*k][Cin_pad32]
+// bf16), the bias padded to Cout_pad16.  cfg6 (nullable): an explicit
+// {MR, NR, G, resw, persist, kind} configuration.
+}  // namespace rv
+extern "C" int rv_conv_bf16(const void* in, int B, int Hin, int Win, int Cin, int in_cs,
+                            const void* w, const float* bias, int Cout, int k, int stride, void* out,
+                            int out_cs, const void* res, int res_cs, int act, const int* cfg6,
+                            void* stream) {
+  using namespace rv;
+  RV_CHECK_ARG(in && w && bias && out, "null pointer");
+  RV_CHECK_ARG(B >= 1 && Hin >= 1 && Win >= 1 && Cin >= 1 && Cout >= 1, "bad shape");
+  RV_CHECK_ARG((k == 1 || k == 3) && (stride == 1 || stride == 2), "k %d stride %d", k, stride);
+  RV_CHECK_ARG(in_cs >= Cin && out_cs >= Cout && (!res || res_cs >= Cout), "channel strides");
+  ConvArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in = (const bf16_t*)in;
+  a.in_cs = in_cs;
+  a.Hin = Hin;
+  a.Win = Win;
+  a.Cin = Cin;
+  a.w = (const bf16_t*)w;
+  a.bias = bias;
+  a.Cout = Cout;
+  a.k = k;
+  a.stride = stride;
+  a.pad = k / 2;
+  a.Ho = (Hin + 2 * a.pad - k) / stride + 1;
+  a.Wo = (Win + 2 * a.pad - k) / stride + 1;
+  a.B = B;
+  a.out0 = out;
+  a.out0_cs = out_cs;
+  a.res = (const bf16_t*)res;
+  a.res_cs = res_cs;
+  a.act = act ? 1 : 0;
+  const hipStream_t s = (hipStream_t)stream;
+  if (cfg6) {
+    const ConvCfg c{cfg6[0], cfg6[1], cfg6[2], cfg6[3], cfg6[4], cfg6[5]};
+    return launch_conv_cfg(a, c, s);
+  }
+  return launch_conv(a, s);
+}
+namespace rv {
 }  // namespace rv

@@ -95,6 +95,9 @@ _SIGS = {
     "rv_yolo_create": (c_int, [c_int, c_void_p, c_int, c_int, c_int, POINTER(c_void_p)]),
     "rv_yolo_destroy": (c_int, [c_void_p]),
     "rv_yolo_set_option": (c_int, [c_void_p, c_int, c_int]),
+    "rv_conv_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                             c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p,
+                             c_void_p]),
     "rv_yolo_packed_bytes2": (c_size_t, [c_int, c_int]),
     "rv_yolo_pack2": (c_int, [c_int, c_int, c_void_p, c_size_t, c_void_p, c_size_t]),
     "rv_yolo_create2": (c_int, [c_int, c_int, c_void_p, c_int, c_int, c_int, POINTER(c_void_p)]),

@@ -296,6 +296,43 @@ def test_stem_cv1_bit_identical_to_unfused_1x1(cuda):
     eng.close()
 
 
+@pytest.mark.parametrize("cfg", [None, (4, 2, 1, 1, 1, 2), (4, 2, 1, 1, 1, 0), (2, 2, 1, 1, 1, 0),
+                                 (4, 1, 1, 0, 1, 2), (2, 4, 1, 1, 1, 0)])
+def test_residual_conv_exact_allocation(cuda, cfg):
+    """A 3x3 bf16 conv + SiLU + residual (the bottleneck form) through
+    rv_conv_bf16 with the residual in its own exactly-sized allocation and
+    Ho, Wo not multiples of any tile height: the deferred-store epilogue
+    (tiles up to 10 fragments) must not read the residual past its end for
+    the bottom tile row's invalid pixels, and the output equals
+    a float64 recomputation to 1 bf16 ulp."""
+    from rvs_amd import _lib
+    B, H, W, C = 2, 37, 45, 64
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn((B, H, W, C), generator=g) * 0.5).to(torch.bfloat16)
+    wt = (torch.randn((C, C, 3, 3), generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(C, generator=g) * 0.1
+    res = (torch.randn((B, H, W, C), generator=g) * 0.5).to(torch.bfloat16)
+    wp = torch.zeros((C, 9, 32 * ((C + 31) // 32)), dtype=torch.bfloat16)
+    wp[:, :, :C] = wt.permute(0, 2, 3, 1).reshape(C, 9, C)
+    xd, wd, bd, rd = x.to(cuda), wp.to(cuda), b.to(cuda), res.to(cuda).clone()
+    out = torch.full((B, H, W, C), float("nan"), dtype=torch.bfloat16, device=cuda)
+    cfg_arr = _lib.int_array(cfg) if cfg is not None else None
+    st = _lib.load().rv_conv_bf16(_lib.ptr(xd), B, H, W, C, C, _lib.ptr(wd), _lib.ptr(bd), C, 3, 1,
+                                  _lib.ptr(out), C, _lib.ptr(rd), C, 1, cfg_arr, _lib.stream_ptr())
+    if cfg is not None and st != 0:
+        pytest.skip(f"configuration {cfg} not valid for this layer")
+    assert st == 0
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), wt.double(), b.double(), padding=1)
+    ref = ref * torch.sigmoid(ref)
+    ref = (ref.permute(0, 2, 3, 1) + res.double()).numpy()
+    got = out.float().cpu().numpy().astype(np.float64)
+    assert np.isfinite(got).all()
+    rms = float(np.sqrt(np.mean(ref ** 2)))
+    d = np.abs(got - ref)
+    assert (d <= 2 * ulp_bf16(ref) + 1e-3 * rms).all()
+
+
 @pytest.mark.parametrize("H,W,B,variant", [(1080, 1920, 3, 0), (640, 640, 1, 0), (360, 640, 2, 0)])
 def test_fused_c2f_is_bit_identical(cuda, H, W, B, variant):
     """The fused C2f chains (c2f.hip: model.2 / model.4 / model.15 bottlenecks
