@@ -164,6 +164,8 @@ __device__ void inv4(const double* S, double* Si) {
 // could not share a workgroup with the association).  Every sum keeps its
 // k order: bit-identical to the whole-matrix form.
 constexpr int kKfP = 0, kKfAP = 49, kKfK = 98, kKfScratch = 126;
+// row-parallel form (kf_update_rows): per detection P | Si | K | AP | y
+constexpr int kKrP = 0, kKrSi = 49, kKrK = 65, kKrAP = 93, kKrY = 142, kKfRows = 147;
 __device__ void kf_update(Track& t, const double z[4], double* sc, int stride) {
   const double R[4] = {1.0, 1.0, 10.0, 10.0};
 #define KF_P(i, j) sc[(kKfP + (i) * 7 + (j)) * stride]
@@ -223,6 +225,80 @@ __device__ void kf_update(Track& t, const double z[4], double* sc, int stride) {
 #undef KF_AP
 #undef KF_K
 #undef KF_A
+}
+
+// kf.update(z) for one matched track by the 8 lanes of one group (lane r
+// of the group owns row r of K, AP and the new P; r = 7 idles in the row
+// phases), on the group's LDS block `sc` (kKfRows doubles).  Every element
+// is the same expression with the same k order as kf_update (bit-identical);
+// only the rows run side by side instead of one after another on one lane.
+// The group's 8 lanes are one 8-lane slice of a wave, so LDS order within
+// the wave plus a wavefront fence between phases is the only sync needed.
+__device__ void kf_update_rows(Track& t, const double z[4], double* sc, int r) {
+  const double R[4] = {1.0, 1.0, 10.0, 10.0};
+#define KR_P(i, j) sc[kKrP + (i) * 7 + (j)]
+#define KR_K(i, j) sc[kKrK + (i) * 4 + (j)]
+#define KR_AP(i, j) sc[kKrAP + (i) * 7 + (j)]
+#define KR_A(i, k) (((i) == (k) ? 1.0 : 0.0) - ((k) < 4 ? KR_K(i, k) : 0.0))
+  auto sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  };
+  for (int e = r; e < 49; e += 8) sc[kKrP + e] = t.P[e];
+  sync();
+  if (r == 0) {
+    double S[16], Si[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sc[kKrY + i] = z[i] - t.x[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) S[i * 4 + j] = KR_P(i, j) + (i == j ? R[i] : 0.0);
+    inv4(S, Si);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sc[kKrSi + e] = Si[e];
+  }
+  sync();
+  if (r < 7) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc += KR_P(r, k) * sc[kKrSi + k * 4 + j];
+      KR_K(r, j) = acc;
+    }
+  }
+  sync();
+  if (r < 7) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc += KR_K(r, k) * sc[kKrY + k];
+    t.x[r] += acc;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      double a2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) a2 += KR_A(r, k) * KR_P(k, j);
+      KR_AP(r, j) = a2;
+    }
+  }
+  sync();
+  if (r < 7) {
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) acc += KR_AP(r, k) * KR_A(j, k);
+      double krk = 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) krk += KR_K(r, k) * R[k] * KR_K(j, k);
+      t.P[r * 7 + j] = acc + krk;
+    }
+  }
+#undef KR_P
+#undef KR_K
+#undef KR_AP
+#undef KR_A
 }
 
 // HomographyProjector.project_point / GroundProjector.distance (track_math.h)
@@ -344,7 +420,9 @@ __host__ __device__ inline size_t sort_assoc_bytes(int tmax, int dmax) {
 }
 __host__ __device__ inline size_t sort_ljob_off(int tmax, int dmax, int kupd) {
   const size_t a = (sort_assoc_bytes(tmax, dmax) + 15) & ~(size_t)15;
-  const size_t b = (size_t)kupd * 126 * 8;  // kKfScratch doubles per update lane
+  // kKfScratch doubles per update lane, or (the row-parallel update, at
+  // most kupd detections) kKfRows doubles per detection
+  const size_t b = (size_t)kupd * (kKfRows > 126 ? kKfRows : 126) * 8;
   return a > b ? a : b;
 }
 
@@ -401,7 +479,7 @@ __device__ __forceinline__ void sort_update_row(Track* __restrict__ pool, const 
                                                 double ts, int s, int d, int2 j, const SortParams& p,
                                                 int* __restrict__ out_id, double* __restrict__ out_dist,
                                                 double* __restrict__ out_speed, double* ap,
-                                                int ap_stride) {
+                                                int ap_stride, bool kf_done = false) {
   const size_t o = (size_t)s * p.dmax + d;
   out_id[o] = -1;
   out_dist[o] = NAN;
@@ -414,9 +492,11 @@ __device__ __forceinline__ void sort_update_row(Track* __restrict__ pool, const 
   const float* de = dets + o * 6;
   Track& tr = pool[(size_t)s * p.tmax + j.x];
   if (j.y < 0) {  // matched: _Track.update + update_metrics
-    double z[4];
-    bbox_to_z(de[0], de[1], de[2], de[3], z);
-    kf_update(tr, z, ap, ap_stride);
+    if (!kf_done) {  // (else kf_update_rows ran it)
+      double z[4];
+      bbox_to_z(de[0], de[1], de[2], de[3], z);
+      kf_update(tr, z, ap, ap_stride);
+    }
     tr.t_pred = ts;
     tr.t_upd = ts;
     tr.hits += 1;
@@ -533,14 +613,24 @@ __global__ __launch_bounds__(NT) void sort_associate_kernel(
     // qualifying pairs appended with one LDS atomic per wave (a ballot's
     // popcount), not one per pair; the append order does not matter (the
     // keys are sorted next and unique)
+    // pair i = tid + kAssocThreads k is (i / D, i % D), stepped
+    // incrementally (an integer division by the runtime D per pair was ~20
+    // VALU, as much as the IoU itself)
+    const int dt = kAssocThreads / D, dd = kAssocThreads - (kAssocThreads / D) * D;
+    int pt = tid / D, pd = tid - (tid / D) * D;
     for (int i0 = 0; i0 < T * D; i0 += kAssocThreads) {
       const int i = i0 + tid;
       bool q = false;
       float v = 0.f;
       if (i < T * D) {
-        const int t = i / D, d = i - (i / D) * D;
-        v = iou_f32(tbox[t], dbox[d]);
+        v = iou_f32(tbox[pt], dbox[pd]);
         q = (double)v >= p.iou_thr;
+      }
+      pt += dt;
+      pd += dd;
+      if (pd >= D) {
+        pd -= D;
+        ++pt;
       }
       const unsigned long long m = __ballot(q);
       if (m) {  // wave-uniform
@@ -739,10 +829,31 @@ __global__ __launch_bounds__(NT) void sort_associate_kernel(
     // states are this block's own global writes, visible after the barrier
     __syncthreads();
     RV_PH(4);  // bookkeeping
-    double* ap = (double*)smem + tid;
-    if (tid < kUpd)
-      for (int d = tid; d < p.dmax; d += kUpd)
-        sort_update_row(pool, dets, ts, s, d, ljob[d], p, out_id, out_dist, out_speed, ap, kUpd);
+    if (D <= NT / 8 && D <= kUpd) {
+      // one 8-lane group per detection: the matched tracks' KF updates row
+      // by row (kf_update_rows), then lane 0 of the group does the rest of
+      // the row (fields, metrics, outputs) as sort_update_row; rows
+      // [D, dmax) get their empty outputs from the lanes beyond
+      const int d = tid >> 3, r = tid & 7;
+      const int2 j = d < D ? ljob[d] : make_int2(-2, -1);
+      const bool matched = d < D && j.x >= 0 && j.y < 0;
+      if (matched) {
+        double z[4];
+        const float* de = dets + ((size_t)s * p.dmax + d) * 6;
+        bbox_to_z(de[0], de[1], de[2], de[3], z);
+        kf_update_rows(pl[j.x], z, (double*)smem + (size_t)d * kKfRows, r);
+      }
+      if (r == 0 && d < D)
+        sort_update_row(pool, dets, ts, s, d, j, p, out_id, out_dist, out_speed, nullptr, 0,
+                        matched);
+      for (int e = D + tid; e < p.dmax; e += NT)
+        sort_update_row(pool, dets, ts, s, e, ljob[e], p, out_id, out_dist, out_speed, nullptr, 0);
+    } else {
+      double* ap = (double*)smem + tid;
+      if (tid < kUpd)
+        for (int d = tid; d < p.dmax; d += kUpd)
+          sort_update_row(pool, dets, ts, s, d, ljob[d], p, out_id, out_dist, out_speed, ap, kUpd);
+    }
     RV_PH(5);  // KF updates + metrics
   }
 }
