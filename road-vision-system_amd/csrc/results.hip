@@ -80,6 +80,22 @@ extern "C" int rv_results_handback(const float* dets, const int* det_n, const in
   const size_t nb = rv_results_bytes(S, dmax);
   RV_CHECK_ARG(stage_bytes >= nb, "stage %zu B < rv_results_bytes = %zu", stage_bytes, nb);
   const int n = S * dmax;
+  // A pinned host record the device can address is written by the pack
+  // kernel itself (one launch; the kernel's completion, which the caller's
+  // event waits for, publishes the writes): no staging copy and no
+  // dependent copy launch per step -- at the end of a pipelined run those
+  // two gaps separated every SORT launch of the drain.  RV_HANDBACK_DIRECT=0
+  // keeps the stage + hipMemcpyAsync form (A/B).
+  static const bool direct = !getenv("RV_HANDBACK_DIRECT") || atoi(getenv("RV_HANDBACK_DIRECT")) != 0;
+  if (host_dst && direct) {
+    void* dptr = nullptr;
+    if (hipHostGetDevicePointer(&dptr, host_dst, 0) == hipSuccess && dptr) {
+      results_pack_kernel<<<ceil_div(n, 256), 256, 0, as_stream(stream)>>>(
+          dets, det_n, track_id, distance_m, speed_kmh, S, dmax, (uint8_t*)dptr);
+      return launch_status("rv_results_handback");
+    }
+    (void)hipGetLastError();  // not a registered host allocation: stage + copy
+  }
   results_pack_kernel<<<ceil_div(n, 256), 256, 0, as_stream(stream)>>>(
       dets, det_n, track_id, distance_m, speed_kmh, S, dmax, (uint8_t*)dev_stage);
   int st = launch_status("rv_results_handback");
