@@ -112,13 +112,19 @@ class YoloEngine:
         self.seg_n = torch.zeros((self.slots, self.max_batch,
                                   max(self.nseg, lib.rv_cand_segments(self.A))),
                                  dtype=torch.int32, device=dev)
-        self.cand_n = torch.zeros(self.max_batch, dtype=torch.int32, device=dev)  # set by NMS
-        # NMS workspace (sort keys of images with more than 4096 candidates)
-        self.nms_ws = torch.empty(max(int(_lib.load().rv_nms_ws_bytes(self.max_batch)), 8),
-                                  dtype=torch.uint8, device=dev)
+        # NMS outputs and workspace (sort keys of images with more than 4096
+        # candidates) per candidate slot: a pipelined engine runs unit u's NMS
+        # beside the SORT steps of unit u-1 (rvs_amd.schedule); the
+        # unsuffixed names are slot 0's
+        self.cand_n_s = torch.zeros((self.slots, self.max_batch), dtype=torch.int32, device=dev)
+        self.nms_ws_s = torch.empty((self.slots, max(int(_lib.load().rv_nms_ws_bytes(self.max_batch)), 8)),
+                                    dtype=torch.uint8, device=dev)
         self._nseg_cur = self.nseg
-        self.dets = torch.zeros((self.max_batch, self.max_det, 6), dtype=torch.float32, device=dev)
-        self.det_n = torch.zeros(self.max_batch, dtype=torch.int32, device=dev)
+        self.dets_s = torch.zeros((self.slots, self.max_batch, self.max_det, 6), dtype=torch.float32,
+                                  device=dev)
+        self.det_n_s = torch.zeros((self.slots, self.max_batch), dtype=torch.int32, device=dev)
+        self.cand_n, self.nms_ws = self.cand_n_s[0], self.nms_ws_s[0]
+        self.dets, self.det_n = self.dets_s[0], self.det_n_s[0]
         gain, px, py = scale_boxes_params((self.in_h, self.in_w), (self.H, self.W))
         self.scale5 = torch.tensor([gain, px, py, self.W, self.H], dtype=torch.float32, device=dev)
         m = class_mask(classes_keep)
@@ -314,13 +320,14 @@ class YoloEngine:
                 call("rv_yolo_set_tuned", h, n, i, _lib.int_array(c))
 
     def nms(self, B: int, slot: int = 0):
-        """NMS + scale_boxes + class filter of candidate slot `slot`."""
+        """NMS + scale_boxes + class filter of candidate slot `slot`, into
+        that slot's outputs."""
         call("rv_nms_postprocess", ptr(self.cand[slot]), ptr(self.seg_n[slot]), B, self.cap,
              self._nseg_cur, self.iou, self.max_det, self.max_nms, self.max_wh, ptr(self.scale5),
              ptr(self.keep),
-             ptr(self.dets), ptr(self.det_n), ptr(self.cand_n), ptr(self.nms_ws),
-             self.nms_ws.numel(), stream_ptr())
-        return self.dets[:B], self.det_n[:B]
+             ptr(self.dets_s[slot]), ptr(self.det_n_s[slot]), ptr(self.cand_n_s[slot]),
+             ptr(self.nms_ws_s[slot]), self.nms_ws_s[slot].numel(), stream_ptr())
+        return self.dets_s[slot][:B], self.det_n_s[slot][:B]
 
     def nms_from_raw(self, raw: torch.Tensor):
         """Reference-layout entry (B, 4+nc, A) -> NMS (parity tests)."""

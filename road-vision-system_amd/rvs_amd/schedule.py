@@ -12,8 +12,9 @@ two ends shorten the pipeline's fill and drain); unit u has four stages
 
     P(u)   preprocess of its P steps into letterbox slot u % 4   (stream sp)
     Y1(u)  first half of its forward on lane u % 2                (stream sy)
-    Y2(u)  second half + decode into candidate slot u % 4         (stream sm)
-    T(u)   NMS, then SORT + result hand-back of each step in order (stream st)
+    Y2(u)  second half + decode into candidate slot u % 4, then
+           that slot's NMS                                       (stream sm)
+    T(u)   SORT + result hand-back of each step in order         (stream st)
 
 ``sync="stage"`` runs them lock-stepped: stage j issues
 Y2(j-1) || P(j+1) || Y1(j) || T(j-2) and joins all four before stage j+1.
@@ -267,6 +268,12 @@ class PipelinedRun:
         # and without the consumer, five A/B pairs; RV_PREP_AFTER_STEM=0 is
         # the r03 order)
         self.prep_after_stem = os.environ.get("RV_PREP_AFTER_STEM", "1") != "0"
+        # unit u's NMS runs on the second-half stream right behind its decode
+        # (per-slot NMS outputs), not at the head of T(u): at the end of a
+        # run it then overlaps the SORT steps of unit u-1 instead of
+        # following them (RV_NMS_ON_Y2=0: the NMS at the head of T(u))
+        self.nms_on_y2 = os.environ.get("RV_NMS_ON_Y2", "1") != "0"
+        self._nms_out = {}
         self.sched = None
         self._events = None
         if mode == "native":
@@ -301,12 +308,18 @@ class PipelinedRun:
     def _y2(self, u: int) -> None:
         slots = self.eng.detector.slots
         self.eng.yolo_stage(None, u % slots, u % 2, part=2, batch=self.units[u] * self.eng.S)
+        if self.nms_on_y2:
+            self._nms_out[u] = self.eng.detector.nms(self.units[u] * self.eng.S, u % slots)
 
     def _track(self, u: int, E: "_Events") -> None:
-        """NMS of the unit's P*S images, then SORT + hand-back of each step
-        in order; a timing event marks each step's completion."""
+        """SORT + hand-back of each step of the unit in order, on the NMS
+        output of its slot (run by Y2(u); RV_NMS_ON_Y2=0: here, first); a
+        timing event marks each step's completion."""
         eng, S, P = self.eng, self.eng.S, self.units[u]
-        dets, det_n = eng.detector.nms(S * P, u % eng.detector.slots)
+        if self.nms_on_y2:
+            dets, det_n = self._nms_out.pop(u)
+        else:
+            dets, det_n = eng.detector.nms(S * P, u % eng.detector.slots)
         for h in range(P):
             k = self.k0[u] + h
             eng.track_handback(dets[h * S:(h + 1) * S], det_n[h * S:(h + 1) * S], self.ts[k],
