@@ -295,11 +295,16 @@ class BenchJob:
         use_pool = os.environ.get("RV_CONSUMER_POOL", "1") != "0"  # A/B probe
         pool = DetectionPool() if materialise and ready is not None and use_pool else None
         want = 8192
-        # A/B probes: RV_CONSUMER_DEFER=1 builds every list after the last
-        # step's hand-back (still inside the timed region); RV_CONSUMER_NOGC=1
-        # keeps the garbage collector off while the lists are built
+        # RV_CONSUMER_DEFER=1 (A/B probe) builds every list after the last
+        # step's hand-back (still inside the timed region).  The cyclic
+        # garbage collector is off while the lists are built (the Detection
+        # objects hold no cycles: reference counting frees them): a
+        # collection triggered by the ~30k new objects of a run stalled the
+        # consumer's last steps by up to 0.6 ms (r06: 4 interleaved rounds,
+        # 46.8k -> 47.4k frames/s, profiles/r06/session_ab/r06ze;
+        # RV_CONSUMER_NOGC=0 leaves it on)
         defer = os.environ.get("RV_CONSUMER_DEFER", "0") != "0"
-        nogc = os.environ.get("RV_CONSUMER_NOGC", "0") != "0"
+        nogc = os.environ.get("RV_CONSUMER_NOGC", "1") != "0"
         if nogc:
             import gc
             gc.disable()
