@@ -1657,7 +1657,11 @@ static bool patch_geo(const ConvArgs& a, const ConvCfg& c, PatchGeo& g, size_t& 
   const int nch = conv_nch(a);
   g.G = std::max(1, std::min(c.G, nch));
   g.fast = epi_fast(a) ? 1 : 0;
-  static const int stagger = getenv("RV_STAGGER") ? atoi(getenv("RV_STAGGER")) : 1;  // A/B switch
+  // the 8-wave stagger (late waves finish a tile beside the partner's
+  // MFMAs): off by default -- measured no gain when built (r06b) and
+  // −1.6 % at the end of r06 (7 interleaved rounds, profiles/r06/session_ab
+  // r06zh / r06zi); RV_STAGGER=1 enables it
+  static const int stagger = getenv("RV_STAGGER") ? atoi(getenv("RV_STAGGER")) : 0;
   g.stagger = stagger;
   // per-lane offset registers of the kernel (patch_maxit)
   const int maxit = (a.stride == 2 ? 6 : 2) * NR + 2;
